@@ -1,0 +1,165 @@
+/*
+ * sfa_hip.h — C ABI of the MI355X (gfx950) hot path of the SFA3D-style
+ * FPN-ResNet-18 LiDAR detector: BEV voxelisation -> KFPN forward -> decode.
+ *
+ * Plain C: pointers, sizes and status codes only; no torch / C++ types.
+ * Every entry point that touches the device takes the caller's hipStream_t
+ * (passed as void*), never allocates, never synchronises, and is re-entrant
+ * per stream; all buffers (including scratch/workspace) are owned by the
+ * caller.  Return value: SFA_OK (0) or a negative SFA_E_* code, with a
+ * human-readable reason in sfa_last_error_string() (thread-local).
+ *
+ * Each entry point names the reference interface it replaces
+ * (paths relative to the reference repository root).
+ */
+#ifndef SFA_HIP_H_
+#define SFA_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SFA_ABI_VERSION 1
+
+enum sfa_status {
+  SFA_OK = 0,
+  SFA_E_INVALID = -1,   /* bad argument / shape */
+  SFA_E_UNSUPPORTED = -2, /* configuration the kernels do not cover */
+  SFA_E_HIP = -3,       /* a HIP runtime call failed */
+  SFA_E_WORKSPACE = -4  /* workspace / scratch too small */
+};
+
+int sfa_abi_version(void);
+const char* sfa_last_error_string(void);
+
+/* ------------------------------------------------------------------ BEV --
+ * Replaces data_process/kitti_data_utils.py:228-251 get_filtered_lidar followed
+ * by data_process/kitti_bev_utils.py:22-55 makeBEVMap, for a batch of frames.
+ *
+ * points          device, float32 [total_points][4] = x, y, z, intensity (raw,
+ *                 unfiltered; the kernel applies the inclusive boundary test)
+ * frame_offsets   HOST, int64 [batch + 1]; frame b = points[off[b], off[b+1])
+ * batch           1 .. SFA_BEV_MAX_BATCH
+ * boundary        HOST, double [6] = minX, maxX, minY, maxY, minZ, maxZ
+ *                 (config/kitti_config.py:23-30)
+ * flags           SFA_BEV_RAW: raw sweep in, the get_filtered_lidar box test and
+ *                 z -= minZ are fused in (the fast path);
+ *                 SFA_BEV_PREFILTERED: points already went through
+ *                 get_filtered_lidar (makeBEVMap's own contract); no box test.
+ * out_layout      SFA_BEV_NCHW3_F32  (B, 3, 608, 608) float32  (== .float() of the
+ *                                    reference's float64 map, test.py:124)
+ *                 SFA_BEV_NCHW3_F64  (B, 3, 608, 608) float64  (reference dtype)
+ *                 SFA_BEV_NHWC4_F32  (B, 608, 608, 4) float32, channel 3 = 0
+ *                                    (the model's input layout; no transpose)
+ * scratch         device, sfa_bev_scratch_size(batch) bytes, ZERO on first use;
+ *                 every call leaves it zeroed again.
+ */
+#define SFA_BEV_MAX_BATCH 64
+enum sfa_bev_layout { SFA_BEV_NCHW3_F32 = 0, SFA_BEV_NCHW3_F64 = 1, SFA_BEV_NHWC4_F32 = 2 };
+enum sfa_bev_flags { SFA_BEV_RAW = 0, SFA_BEV_PREFILTERED = 1 };
+
+size_t sfa_bev_scratch_size(int batch);
+int sfa_bev_voxelize(const float* points, const int64_t* frame_offsets, int batch,
+                     const double* boundary, int flags, int out_layout, void* out, void* scratch,
+                     void* stream);
+
+/* Replaces data_process/kitti_data_utils.py:228-251 get_filtered_lidar (labels=None):
+ * order-preserving compaction of the points inside the inclusive box, with
+ * z <- z - minZ.  points/out device float32 [n][4]; out must hold n points;
+ * *out_count (DEVICE int64) receives the kept count.  scratch: device,
+ * sfa_filter_scratch_size(n) bytes. */
+size_t sfa_filter_scratch_size(int64_t n_points);
+int sfa_filter_points(const float* points, int64_t n_points, const double* boundary, float* out,
+                      int64_t* out_count, void* scratch, size_t scratch_bytes, void* stream);
+
+/* ---------------------------------------------------------------- model --
+ * Replaces models/model_utils.py:25-43 create_model -> models/fpn_resnet.py
+ * get_pose_net(18, heads, 64) (:296-301) and PoseResNet.forward (:169-246).
+ *
+ * Architecture descriptor: resnet depth (18 only), head_conv (64 only) and the
+ * heads in FORWARD order (the `heads` dict insertion order, fpn_resnet.py:220);
+ * the state_dict registers them in sorted() order (fpn_resnet.py:135).
+ */
+#define SFA_MAX_HEADS 8
+typedef struct sfa_arch {
+  int num_layers;                 /* 18 */
+  int head_conv;                  /* 64 */
+  int num_heads;                  /* 1 .. SFA_MAX_HEADS */
+  int head_channels[SFA_MAX_HEADS]; /* 1 .. 4 each, forward order */
+  char head_names[SFA_MAX_HEADS][32];
+} sfa_arch;
+
+/* Reference state_dict layout (186 entries for fpn_resnet_18 with 5 heads), in
+ * nn.Module registration order.  shape is padded with 0s; ndim 0 = scalar. */
+int sfa_state_count(const sfa_arch* arch);
+int sfa_state_entry(const sfa_arch* arch, int index, char* name, int name_len, int64_t* shape4,
+                    int* ndim);
+
+/* Pack weights (host -> host): `state` = the float32 values of every
+ * state_dict entry except *.num_batches_tracked, concatenated in
+ * sfa_state_entry order.  BatchNorm (eps 1e-5) is folded into the preceding
+ * convolution; conv weights are re-laid out OHWI / K-concatenated for the
+ * implicit-GEMM kernels.  `packed` must hold sfa_packed_floats(arch) floats. */
+size_t sfa_state_floats(const sfa_arch* arch);
+size_t sfa_packed_floats(const sfa_arch* arch);
+int sfa_pack_weights(const sfa_arch* arch, const float* state, size_t state_floats, float* packed);
+
+/* A model handle references a device copy of the packed weights (caller-owned,
+ * must outlive the handle).  No device memory is allocated. */
+typedef struct sfa_model sfa_model;
+int sfa_model_create(const sfa_arch* arch, const float* packed_device, sfa_model** out);
+void sfa_model_destroy(sfa_model* model);
+
+/* Forward.  x: device float32, layout SFA_IN_NCHW3 (B,3,H,W) as the reference
+ * takes it, or SFA_IN_NHWC4 (B,H,W,4) as sfa_bev_voxelize writes it.
+ * H, W multiples of 32.  head_out[i]: device float32 (B, c_i, H/4, W/4) NCHW,
+ * contiguous, forward head order — raw logits like the reference (no sigmoid).
+ * workspace: sfa_forward_workspace_size(B, H, W) bytes. */
+enum sfa_input_layout { SFA_IN_NCHW3 = 0, SFA_IN_NHWC4 = 1 };
+size_t sfa_forward_workspace_size(const sfa_model* model, int batch, int height, int width);
+int sfa_model_forward(const sfa_model* model, const float* x, int in_layout, int batch, int height,
+                      int width, float* const* head_out, void* workspace, size_t workspace_bytes,
+                      void* stream);
+
+/* Byte offset inside the forward workspace of an intermediate map, valid after
+ * sfa_model_forward returns on the stream (for the reference's opt-in
+ * visualisation capture, fpn_resnet.py:189-242).  LAYERk / UP_LEVELk are NHWC
+ * float32 (B, h, w, C); HEADS_Lk are channel-planar float32
+ * [sum(head_channels)][B][h][w] per KFPN level.  -1 on bad arguments. */
+enum sfa_buffer {
+  SFA_BUF_LAYER1 = 0, SFA_BUF_LAYER2, SFA_BUF_LAYER3, SFA_BUF_LAYER4,
+  SFA_BUF_UP_LEVEL2, SFA_BUF_UP_LEVEL3, SFA_BUF_UP_LEVEL4,
+  SFA_BUF_HEADS_L0, SFA_BUF_HEADS_L1, SFA_BUF_HEADS_L2
+};
+int64_t sfa_forward_buffer_offset(const sfa_model* model, int batch, int height, int width,
+                                  int which);
+
+/* --------------------------------------------------------------- decode --
+ * Replaces utils/torch_utils.py:44-45 _sigmoid (in place: sigmoid then
+ * clamp(1e-4, 1-1e-4)). */
+int sfa_sigmoid_clamp_inplace(float* x, int64_t n, void* stream);
+
+/* Replaces utils/evaluation_utils.py:77-105 decode (with _nms :21-26, _topk
+ * :47-62, _transpose_and_gather_feat :40-44).  All maps device float32 NCHW
+ * contiguous: hm (B,C,H,W), off (B,2,H,W) or NULL, dir (B,2,H,W),
+ * z (B,1,H,W), dim (B,3,H,W).  apply_sigmoid != 0 applies _sigmoid to hm and
+ * off on the fly (the test.py:150,167 pair) without modifying them.
+ * dets: device float32 (B, K, 10) columns
+ *   [score, xs+off0, ys+off1, z, dim0, dim1, dim2, dir0, dir1, class].
+ * Ties (unspecified order in torch.topk) break by lower flat index, then lower
+ * class.  Constraints: K <= 256, K <= H*W, H*W <= 36864, C <= 16.
+ * workspace: sfa_decode_workspace_size(B, C, K) bytes. */
+size_t sfa_decode_workspace_size(int batch, int num_classes, int K);
+int sfa_decode(const float* hm, const float* off, const float* dir, const float* z,
+               const float* dim, int batch, int num_classes, int height, int width, int K,
+               int apply_sigmoid, float* dets, void* workspace, size_t workspace_bytes,
+               void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SFA_HIP_H_ */

@@ -1,0 +1,22 @@
+#pragma once
+
+#include "common.h"
+
+namespace sfa {
+
+struct KfpnOut {
+  float* ptr[SFA_MAX_HEADS];  // NCHW (B, ch[j], h, w) per head, forward order
+  int ch[SFA_MAX_HEADS];
+  int off[SFA_MAX_HEADS];     // first planar channel of head j
+  int num_heads;
+  int total_ch;
+};
+
+int launch_nchw3_to_nhwc4(const float* x, float* y, int B, int H, int W, hipStream_t st);
+int launch_maxpool3s2(const float* x, float* y, int B, int H, int W, int C, hipStream_t st);
+int launch_upsample2x(const float* x, float* y, int B, int H, int W, int C, hipStream_t st);
+int launch_kfpn(const float* L0, const float* L1, const float* L2, const KfpnOut& o, int B, int h,
+                int w, hipStream_t st);
+int launch_sigmoid_clamp(float* x, long long n, hipStream_t st);
+
+}  // namespace sfa

@@ -1,0 +1,188 @@
+// Memory-bound helpers of the forward (HBM roofline; NHWC, float4 per lane).
+//   nchw3_to_nhwc4      API input (B,3,H,W) -> (B,H,W,4)        test.py:124 boundary
+//   maxpool3s2          fpn_resnet.py:123,182  MaxPool2d(3, 2, 1), -inf padding
+//   upsample2x_bilinear fpn_resnet.py:198,202,207  F.interpolate(x2, bilinear, align_corners=True)
+//   kfpn_combine        fpn_resnet.py:224-254  nearest-resize level 0, softmax over 3 levels,
+//                       sum(v * softmax(v)), written NCHW per head
+//   sigmoid_clamp       utils/torch_utils.py:44-45
+#include "aux_kernels.h"
+
+namespace sfa {
+
+__global__ void __launch_bounds__(256) nchw3_to_nhwc4_kernel(const float* __restrict__ x,
+                                                             float4* __restrict__ y, int B, int HW) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long long)B * HW) return;
+  const int b = (int)(i / HW), p = (int)(i - (long long)b * HW);
+  const float* s = x + (size_t)b * 3 * HW + p;
+  y[i] = make_float4(s[0], s[HW], s[2 * HW], 0.f);
+}
+
+// One thread per (output pixel, 4 channels).
+__global__ void __launch_bounds__(256) maxpool3s2_kernel(const float4* __restrict__ x,
+                                                         float4* __restrict__ y, int B, int H, int W,
+                                                         int C4, int OH, int OW) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)B * OH * OW * C4;
+  if (i >= total) return;
+  const int c = (int)(i % C4);
+  long long t = i / C4;
+  const int ox = (int)(t % OW);
+  t /= OW;
+  const int oy = (int)(t % OH);
+  const int b = (int)(t / OH);
+  float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const int iy = oy * 2 - 1 + dy;
+    if ((unsigned)iy >= (unsigned)H) continue;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int ix = ox * 2 - 1 + dx;
+      if ((unsigned)ix >= (unsigned)W) continue;
+      const float4 v = x[(((size_t)b * H + iy) * W + ix) * C4 + c];
+      m.x = fmaxf(m.x, v.x);
+      m.y = fmaxf(m.y, v.y);
+      m.z = fmaxf(m.z, v.z);
+      m.w = fmaxf(m.w, v.w);
+    }
+  }
+  y[i] = m;
+}
+
+// align_corners=True: src = dst * (in-1)/(out-1) in f32 (ATen area_pixel_compute_scale /
+// _source_index), i0 = floor(src), i1 = i0 + (i0 < in-1), l1 = src - i0, l0 = 1 - l1.
+__global__ void __launch_bounds__(256) upsample2x_bilinear_kernel(const float4* __restrict__ x,
+                                                                  float4* __restrict__ y, int B,
+                                                                  int H, int W, int C4, float sh,
+                                                                  float sw) {
+  const int OH = 2 * H, OW = 2 * W;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)B * OH * OW * C4;
+  if (i >= total) return;
+  const int c = (int)(i % C4);
+  long long t = i / C4;
+  const int ox = (int)(t % OW);
+  t /= OW;
+  const int oy = (int)(t % OH);
+  const int b = (int)(t / OH);
+  const float fy = sh * (float)oy, fx = sw * (float)ox;
+  const int y0 = (int)fy, x0 = (int)fx;
+  const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+  const float ly1 = fy - (float)y0, lx1 = fx - (float)x0;
+  const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+  const size_t base = (size_t)b * H;
+  const float4 a00 = x[((base + y0) * W + x0) * C4 + c];
+  const float4 a01 = x[((base + y0) * W + x1) * C4 + c];
+  const float4 a10 = x[((base + y1) * W + x0) * C4 + c];
+  const float4 a11 = x[((base + y1) * W + x1) * C4 + c];
+  float4 o;
+  o.x = ly0 * (lx0 * a00.x + lx1 * a01.x) + ly1 * (lx0 * a10.x + lx1 * a11.x);
+  o.y = ly0 * (lx0 * a00.y + lx1 * a01.y) + ly1 * (lx0 * a10.y + lx1 * a11.y);
+  o.z = ly0 * (lx0 * a00.z + lx1 * a01.z) + ly1 * (lx0 * a10.z + lx1 * a11.z);
+  o.w = ly0 * (lx0 * a00.w + lx1 * a01.w) + ly1 * (lx0 * a10.w + lx1 * a11.w);
+  y[i] = o;
+}
+
+// Planar level buffers: Lk[ch][b][y][x] (ch over all heads, forward order).
+// Level 0 is at (h/2, w/2) and resized by nearest (src = dst // 2, F.interpolate
+// default mode with an exact 0.5 scale).
+__global__ void __launch_bounds__(256) kfpn_combine_kernel(const float* __restrict__ L0,
+                                                           const float* __restrict__ L1,
+                                                           const float* __restrict__ L2,
+                                                           KfpnOut o, int B, int h, int w) {
+  const int hw = h * w;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long total = (long long)o.total_ch * B * hw;
+  if (i >= total) return;
+  const int ch = (int)(i / ((long long)B * hw));
+  const int rem = (int)(i - (long long)ch * B * hw);
+  const int b = rem / hw;
+  const int p = rem - b * hw;
+  const int yy = p / w, xx = p - yy * w;
+  const int h0 = h / 2, w0 = w / 2;
+  const float v0 = L0[((size_t)ch * B + b) * (h0 * w0) + (yy >> 1) * w0 + (xx >> 1)];
+  const float v1 = L1[((size_t)ch * B + b) * hw + p];
+  const float v2 = L2[((size_t)ch * B + b) * hw + p];
+  // softmax over the stacked last dim (torch: max-subtract, exp, sum, divide).
+  const float mx = fmaxf(fmaxf(v0, v1), v2);
+  const float e0 = expf(v0 - mx), e1 = expf(v1 - mx), e2 = expf(v2 - mx);
+  const float sum = e0 + e1 + e2;
+  const float w0_ = e0 / sum, w1_ = e1 / sum, w2_ = e2 / sum;
+  const float r = v0 * w0_ + v1 * w1_ + v2 * w2_;
+  // head of this channel
+  int hd = 0;
+#pragma unroll
+  for (int j = 1; j < SFA_MAX_HEADS; ++j)
+    if (j < o.num_heads && ch >= o.off[j]) hd = j;
+  float* dst = o.ptr[0];
+  int nc = o.ch[0];
+#pragma unroll
+  for (int j = 1; j < SFA_MAX_HEADS; ++j)
+    if (j == hd) {
+      dst = o.ptr[j];
+      nc = o.ch[j];
+    }
+  const int c = ch - o.off[hd];
+  dst[((size_t)b * nc + c) * hw + p] = r;
+}
+
+__global__ void __launch_bounds__(256) sigmoid_clamp_kernel(float* __restrict__ x, long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float s = 1.0f / (1.0f + expf(-x[i]));
+  x[i] = fminf(fmaxf(s, 1e-4f), 1.0f - 1e-4f);
+}
+
+static unsigned grid_of(long long n) { return (unsigned)((n + 255) / 256); }
+
+int launch_nchw3_to_nhwc4(const float* x, float* y, int B, int H, int W, hipStream_t st) {
+  const long long n = (long long)B * H * W;
+  hipLaunchKernelGGL(nchw3_to_nhwc4_kernel, dim3(grid_of(n)), dim3(256), 0, st, x,
+                     reinterpret_cast<float4*>(y), B, H * W);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+int launch_maxpool3s2(const float* x, float* y, int B, int H, int W, int C, hipStream_t st) {
+  const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
+  const long long n = (long long)B * OH * OW * (C / 4);
+  hipLaunchKernelGGL(maxpool3s2_kernel, dim3(grid_of(n)), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), B, H, W, C / 4,
+                     OH, OW);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+int launch_upsample2x(const float* x, float* y, int B, int H, int W, int C, hipStream_t st) {
+  const float sh = H > 1 ? (float)(H - 1) / (float)(2 * H - 1) : 0.f;
+  const float sw = W > 1 ? (float)(W - 1) / (float)(2 * W - 1) : 0.f;
+  const long long n = (long long)B * 4 * H * W * (C / 4);
+  hipLaunchKernelGGL(upsample2x_bilinear_kernel, dim3(grid_of(n)), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), B, H, W, C / 4,
+                     sh, sw);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+int launch_kfpn(const float* L0, const float* L1, const float* L2, const KfpnOut& o, int B, int h,
+                int w, hipStream_t st) {
+  const long long n = (long long)o.total_ch * B * h * w;
+  hipLaunchKernelGGL(kfpn_combine_kernel, dim3(grid_of(n)), dim3(256), 0, st, L0, L1, L2, o, B, h, w);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+int launch_sigmoid_clamp(float* x, long long n, hipStream_t st) {
+  if (n <= 0) return SFA_OK;
+  hipLaunchKernelGGL(sigmoid_clamp_kernel, dim3(grid_of(n)), dim3(256), 0, st, x, n);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+}  // namespace sfa
+
+extern "C" int sfa_sigmoid_clamp_inplace(float* x, int64_t n, void* stream) {
+  SFA_CHECK_ARG(n >= 0 && (n == 0 || x), "sigmoid: bad arguments");
+  return sfa::launch_sigmoid_clamp(x, n, reinterpret_cast<hipStream_t>(stream));
+}

@@ -1,0 +1,333 @@
+// BEV voxelisation: get_filtered_lidar + makeBEVMap on the GPU.
+//
+// Reference: data_process/kitti_data_utils.py:228-251 (filter),
+//            data_process/kitti_bev_utils.py:22-55 (makeBEVMap).
+//
+// Two passes, HBM/atomic bound (SURVEY §8(a) row a1'):
+//   pass 1 (one thread per point): inclusive f32 box test, z' = z - minZ (f32),
+//     cell = (floor(x/D), trunc(floor(y/D) + 304.5)) with IEEE f32 division,
+//     atomicMax of a 64-bit key (bits(z') << 32 | ~index) — z' >= +0 so the
+//     float bits are monotone; the max key is the max z with ties broken by the
+//     FIRST point in input order, exactly the row np.unique(return_index) picks
+//     after the stable lexsort((-z, col, row)) — and atomicAdd of the count.
+//   pass 2 (one thread per BEV cell): intensity = i[top], height = z'/4.0 (f32),
+//     density = min(1, ln(count+1)/ln 64) (f64 table), written in the requested
+//     layout; the scratch cell is re-zeroed for the next call.
+// The result is independent of atomic arrival order: bit-exact.
+#include "common.h"
+
+namespace sfa {
+
+constexpr int kBevH = 608;
+constexpr int kBevW = 608;
+constexpr int kBevCells = kBevH * kBevW;
+
+struct BevArgs {
+  int64_t start[SFA_BEV_MAX_BATCH + 1];
+  float minX, maxX, minY, maxY, minZ, maxZ;
+  float disc;        // f32(50/608)
+  float half_w;      // (BEV_W + 1) / 2 = 304.5
+  float max_height;  // f32(float(abs(maxZ - minZ)))
+  double density[64];  // min(1, ln(c+1)/ln 64), c = 0..63 (c >= 63 -> 1)
+};
+
+template <bool RAW>
+__global__ void __launch_bounds__(256) bev_scatter_kernel(const float4* __restrict__ pts,
+                                                          BevArgs a,
+                                                          unsigned long long* __restrict__ keys,
+                                                          unsigned* __restrict__ counts) {
+  const int b = blockIdx.y;
+  const int64_t s = a.start[b];
+  const int64_t n = a.start[b + 1] - s;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 p = pts[s + i];
+  float zr = p.z;
+  if (RAW) {
+    // kitti_data_utils.py:237-239 — inclusive on both ends, NaN fails.
+    if (!(p.x >= a.minX && p.x <= a.maxX && p.y >= a.minY && p.y <= a.maxY && p.z >= a.minZ &&
+          p.z <= a.maxZ))
+      return;
+    zr = __fsub_rn(p.z, a.minZ);  // :241
+  } else if (!(zr >= 0.f)) {
+    // makeBEVMap on already-filtered points: z is >= 0 after the filter; a negative or
+    // NaN z has no defined top-point order (the 64-bit key needs z >= +0) -> skipped.
+    return;
+  }
+  int row = (int)floorf(__fdiv_rn(p.x, a.disc));                      // kitti_bev_utils.py:28
+  int col = (int)__fadd_rn(floorf(__fdiv_rn(p.y, a.disc)), a.half_w);  // :29 (np.int_ truncates)
+  // numpy fancy indexing wraps negative indices of the (609, 609) maps (:44-48).
+  if (row < 0) row += kBevH + 1;
+  if (col < 0) col += kBevW + 1;
+  // :50-53 crop to [:608, :608]; indices outside the (609, 609) table (IndexError in
+  // numpy) cannot occur after the filter and are skipped for pre-filtered input.
+  if (row < 0 || row >= kBevH || col < 0 || col >= kBevW) return;
+  const int cell = row * kBevW + col;
+  const unsigned long long key =
+      ((unsigned long long)__float_as_uint(zr) << 32) | (unsigned)(~(unsigned)i);
+  unsigned long long* kp = keys + (size_t)b * kBevCells + cell;
+  atomicMax(kp, key);
+  atomicAdd(counts + (size_t)b * kBevCells + cell, 1u);
+}
+
+template <int LAYOUT>
+__global__ void __launch_bounds__(256) bev_gather_kernel(const float4* __restrict__ pts, BevArgs a,
+                                                         unsigned long long* __restrict__ keys,
+                                                         unsigned* __restrict__ counts,
+                                                         void* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int cell = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cell >= kBevCells) return;
+  const size_t sc = (size_t)b * kBevCells + cell;
+  const unsigned cnt = counts[sc];
+  float inten = 0.f, height = 0.f;
+  double dens = 0.0;
+  if (cnt) {
+    const unsigned long long key = keys[sc];
+    const unsigned idx = ~(unsigned)(key & 0xffffffffull);
+    const float zr = __uint_as_float((unsigned)(key >> 32));
+    inten = pts[a.start[b] + idx].w;
+    height = __fdiv_rn(zr, a.max_height);  // :43-44, f32 division
+    dens = a.density[cnt < 63u ? cnt : 63u];
+    keys[sc] = 0ull;  // leave scratch zeroed for the next call
+    counts[sc] = 0u;
+  }
+  if (LAYOUT == SFA_BEV_NHWC4_F32) {
+    float4 v = make_float4(inten, height, (float)dens, 0.f);
+    reinterpret_cast<float4*>(out)[sc] = v;
+  } else if (LAYOUT == SFA_BEV_NCHW3_F32) {
+    float* o = reinterpret_cast<float*>(out) + (size_t)b * 3 * kBevCells + cell;
+    o[0] = inten;
+    o[kBevCells] = height;
+    o[2 * kBevCells] = (float)dens;
+  } else {
+    double* o = reinterpret_cast<double*>(out) + (size_t)b * 3 * kBevCells + cell;
+    o[0] = (double)inten;
+    o[kBevCells] = (double)height;
+    o[2 * kBevCells] = dens;
+  }
+}
+
+}  // namespace sfa
+
+using namespace sfa;
+
+extern "C" size_t sfa_bev_scratch_size(int batch) {
+  if (batch <= 0) return 0;
+  return align_up((size_t)batch * kBevCells * sizeof(unsigned long long), 256) +
+         align_up((size_t)batch * kBevCells * sizeof(unsigned), 256);
+}
+
+extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offsets, int batch,
+                                const double* boundary, int flags, int out_layout, void* out,
+                                void* scratch, void* stream) {
+  SFA_CHECK_ARG(batch >= 1 && batch <= SFA_BEV_MAX_BATCH, "bev: batch %d out of [1, %d]", batch,
+                SFA_BEV_MAX_BATCH);
+  SFA_CHECK_ARG(frame_offsets && boundary && out && scratch, "bev: null argument");
+  SFA_CHECK_ARG(out_layout >= 0 && out_layout <= 2, "bev: bad out_layout %d", out_layout);
+  SFA_CHECK_ARG(flags == SFA_BEV_RAW || flags == SFA_BEV_PREFILTERED, "bev: bad flags %d", flags);
+  BevArgs a;
+  int64_t max_n = 0;
+  for (int b = 0; b <= batch; ++b) {
+    a.start[b] = frame_offsets[b];
+    if (b > 0) {
+      const int64_t n = frame_offsets[b] - frame_offsets[b - 1];
+      SFA_CHECK_ARG(n >= 0, "bev: frame_offsets not monotone at %d", b);
+      SFA_CHECK_ARG(n < (int64_t)0xffffffff, "bev: frame %d has too many points", b - 1);
+      if (n > max_n) max_n = n;
+    }
+  }
+  SFA_CHECK_ARG(frame_offsets[0] >= 0, "bev: negative frame offset");
+  SFA_CHECK_ARG(max_n == 0 || points, "bev: null points");
+  // Python floats -> f32 as numpy does for f32-array ops (NEP 50 / numpy 1.18 agree).
+  a.minX = (float)boundary[0];
+  a.maxX = (float)boundary[1];
+  a.minY = (float)boundary[2];
+  a.maxY = (float)boundary[3];
+  a.minZ = (float)boundary[4];
+  a.maxZ = (float)boundary[5];
+  a.disc = (float)(50.0 / 608.0);  // config/kitti_config.py:47
+  a.half_w = 304.5f;
+  a.max_height = (float)std::fabs(boundary[5] - boundary[4]);
+  for (int c = 0; c < 64; ++c) {
+    double v = std::log((double)c + 1.0) / std::log(64.0);
+    a.density[c] = c == 0 ? 0.0 : (v < 1.0 ? v : 1.0);
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  auto* keys = reinterpret_cast<unsigned long long*>(scratch);
+  auto* counts = reinterpret_cast<unsigned*>(
+      reinterpret_cast<char*>(scratch) +
+      align_up((size_t)batch * kBevCells * sizeof(unsigned long long), 256));
+  const float4* p4 = reinterpret_cast<const float4*>(points);
+  if (max_n > 0) {
+    dim3 g1((unsigned)((max_n + 255) / 256), batch);
+    if (flags == SFA_BEV_RAW)
+      hipLaunchKernelGGL(bev_scatter_kernel<true>, g1, dim3(256), 0, st, p4, a, keys, counts);
+    else
+      hipLaunchKernelGGL(bev_scatter_kernel<false>, g1, dim3(256), 0, st, p4, a, keys, counts);
+    SFA_LAUNCH_CHECK();
+  }
+  dim3 g2((unsigned)ceil_div(kBevCells, 256), batch);
+  switch (out_layout) {
+    case SFA_BEV_NCHW3_F32:
+      hipLaunchKernelGGL(bev_gather_kernel<SFA_BEV_NCHW3_F32>, g2, dim3(256), 0, st, p4, a, keys,
+                         counts, out);
+      break;
+    case SFA_BEV_NCHW3_F64:
+      hipLaunchKernelGGL(bev_gather_kernel<SFA_BEV_NCHW3_F64>, g2, dim3(256), 0, st, p4, a, keys,
+                         counts, out);
+      break;
+    default:
+      hipLaunchKernelGGL(bev_gather_kernel<SFA_BEV_NHWC4_F32>, g2, dim3(256), 0, st, p4, a, keys,
+                         counts, out);
+  }
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+// ---------------------------------------------------------------- filter --
+// get_filtered_lidar (kitti_data_utils.py:228-251) as an order-preserving stream
+// compaction: per-block keep counts -> one-block exclusive scan -> scatter with
+// an in-block scan over contiguous per-thread ranges.
+namespace sfa {
+
+constexpr int kFiltThreads = 256;
+constexpr int kFiltItems = 8;
+constexpr int kFiltChunk = kFiltThreads * kFiltItems;
+
+struct FiltArgs {
+  float minX, maxX, minY, maxY, minZ, maxZ;
+};
+
+__device__ __forceinline__ bool keep_point(const float4& p, const FiltArgs& f) {
+  return p.x >= f.minX && p.x <= f.maxX && p.y >= f.minY && p.y <= f.maxY && p.z >= f.minZ &&
+         p.z <= f.maxZ;
+}
+
+__device__ int block_scan256(int v, int* sh /*[4]*/, int* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[wave] = x;
+  __syncthreads();
+  int before = 0;
+  for (int w = 0; w < wave; ++w) before += sh[w];
+  *total = sh[0] + sh[1] + sh[2] + sh[3];
+  __syncthreads();
+  return before + x - v;
+}
+
+__global__ void __launch_bounds__(kFiltThreads) filter_count_kernel(const float4* __restrict__ pts,
+                                                                    long long n, FiltArgs f,
+                                                                    int* __restrict__ bcount) {
+  __shared__ int sh[4];
+  const long long base = (long long)blockIdx.x * kFiltChunk + (long long)threadIdx.x * kFiltItems;
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < kFiltItems; ++j)
+    if (base + j < n) c += keep_point(pts[base + j], f);
+  int total;
+  block_scan256(c, sh, &total);
+  if (threadIdx.x == 0) bcount[blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(1024) filter_scan_kernel(int* __restrict__ bcount, int nb,
+                                                           long long* __restrict__ out_n) {
+  __shared__ int wsum[16];
+  __shared__ long long carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int base = 0; base < nb; base += 1024) {
+    const int i = base + threadIdx.x;
+    const int v = i < nb ? bcount[i] : 0;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    int before = 0;
+    for (int w = 0; w < wave; ++w) before += wsum[w];
+    int tot = 0;
+    for (int w = 0; w < 16; ++w) tot += wsum[w];
+    if (i < nb) bcount[i] = (int)(carry + before + x - v);
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out_n = carry;
+}
+
+__global__ void __launch_bounds__(kFiltThreads) filter_scatter_kernel(
+    const float4* __restrict__ pts, long long n, FiltArgs f, const int* __restrict__ boff,
+    float4* __restrict__ out) {
+  __shared__ int sh[4];
+  const long long base = (long long)blockIdx.x * kFiltChunk + (long long)threadIdx.x * kFiltItems;
+  float4 v[kFiltItems];
+  bool k[kFiltItems];
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < kFiltItems; ++j) {
+    k[j] = false;
+    if (base + j < n) {
+      v[j] = pts[base + j];
+      k[j] = keep_point(v[j], f);
+    }
+    c += k[j];
+  }
+  int total;
+  int pos = boff[blockIdx.x] + block_scan256(c, sh, &total);
+#pragma unroll
+  for (int j = 0; j < kFiltItems; ++j)
+    if (k[j]) {
+      float4 q = v[j];
+      q.z = __fsub_rn(q.z, f.minZ);  // :241
+      out[pos++] = q;
+    }
+}
+
+}  // namespace sfa
+
+extern "C" size_t sfa_filter_scratch_size(int64_t n_points) {
+  const long long nb = (n_points + kFiltChunk - 1) / kFiltChunk;
+  return align_up((size_t)(nb > 0 ? nb : 1) * sizeof(int), 256) + 256;
+}
+
+extern "C" int sfa_filter_points(const float* points, int64_t n_points, const double* boundary,
+                                 float* out, int64_t* out_count, void* scratch,
+                                 size_t scratch_bytes, void* stream) {
+  SFA_CHECK_ARG(n_points >= 0 && boundary && out_count && scratch, "filter: bad arguments");
+  SFA_CHECK_ARG(n_points == 0 || (points && out), "filter: null points");
+  SFA_CHECK_ARG(n_points < (1ll << 31) * (long long)kFiltChunk / 4, "filter: too many points");
+  if (scratch_bytes < sfa_filter_scratch_size(n_points)) {
+    set_error("filter: scratch too small");
+    return SFA_E_WORKSPACE;
+  }
+  FiltArgs f{(float)boundary[0], (float)boundary[1], (float)boundary[2],
+             (float)boundary[3], (float)boundary[4], (float)boundary[5]};
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int nb = (int)((n_points + kFiltChunk - 1) / kFiltChunk);
+  int* bcount = reinterpret_cast<int*>(scratch);
+  const float4* p4 = reinterpret_cast<const float4*>(points);
+  if (nb == 0) {
+    SFA_HIP_TRY(hipMemsetAsync(out_count, 0, sizeof(int64_t), st));
+    return SFA_OK;
+  }
+  hipLaunchKernelGGL(filter_count_kernel, dim3(nb), dim3(kFiltThreads), 0, st, p4,
+                     (long long)n_points, f, bcount);
+  SFA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(filter_scan_kernel, dim3(1), dim3(1024), 0, st, bcount, nb,
+                     reinterpret_cast<long long*>(out_count));
+  SFA_LAUNCH_CHECK();
+  hipLaunchKernelGGL(filter_scatter_kernel, dim3(nb), dim3(kFiltThreads), 0, st, p4,
+                     (long long)n_points, f, bcount, reinterpret_cast<float4*>(out));
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}

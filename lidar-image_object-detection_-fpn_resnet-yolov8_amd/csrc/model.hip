@@ -1,0 +1,608 @@
+// FPN-ResNet-18 (KFPN) model: reference state_dict layout, host-side weight
+// packing (BatchNorm folding + OHWI re-layout) and the forward orchestration.
+//
+// Reference: models/fpn_resnet.py:112-301 (PoseResNet, BasicBlock, get_pose_net),
+//            models/model_utils.py:25-43 (create_model).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "aux_kernels.h"
+#include "conv.h"
+
+namespace sfa {
+
+static thread_local std::string g_err;
+
+void set_error(const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+}
+
+struct Entry {
+  std::string name;
+  std::vector<int64_t> shape;
+};
+
+static int64_t numel(const Entry& e) {
+  int64_t n = 1;
+  for (auto s : e.shape) n *= s;
+  return n;
+}
+
+static const int kFpnC[3] = {256, 128, 64};
+
+static int check_arch(const sfa_arch* a) {
+  SFA_CHECK_ARG(a != nullptr, "arch is null");
+  if (a->num_layers != 18) {
+    set_error("only fpn_resnet_18 is implemented (got %d layers)", a->num_layers);
+    return SFA_E_UNSUPPORTED;
+  }
+  if (a->head_conv != 64) {
+    set_error("only head_conv = 64 is implemented (got %d)", a->head_conv);
+    return SFA_E_UNSUPPORTED;
+  }
+  SFA_CHECK_ARG(a->num_heads >= 1 && a->num_heads <= SFA_MAX_HEADS, "num_heads %d out of range",
+                a->num_heads);
+  for (int j = 0; j < a->num_heads; ++j) {
+    SFA_CHECK_ARG(a->head_channels[j] >= 1 && a->head_channels[j] <= 4,
+                  "head %d: channels %d out of [1, 4]", j, a->head_channels[j]);
+    SFA_CHECK_ARG(strnlen(a->head_names[j], 32) > 0 && strnlen(a->head_names[j], 32) < 32,
+                  "head %d: bad name", j);
+  }
+  return SFA_OK;
+}
+
+static std::vector<int> sorted_heads(const sfa_arch* a) {
+  std::vector<int> idx(a->num_heads);
+  for (int j = 0; j < a->num_heads; ++j) idx[j] = j;
+  std::sort(idx.begin(), idx.end(), [&](int x, int y) {
+    return std::string(a->head_names[x]) < std::string(a->head_names[y]);
+  });
+  return idx;
+}
+
+// nn.Module registration order of PoseResNet (fpn_resnet.py:114-151, 42-53).
+static std::vector<Entry> state_layout(const sfa_arch* a) {
+  std::vector<Entry> v;
+  auto bn = [&](const std::string& p, int64_t c) {
+    v.push_back({p + ".weight", {c}});
+    v.push_back({p + ".bias", {c}});
+    v.push_back({p + ".running_mean", {c}});
+    v.push_back({p + ".running_var", {c}});
+    v.push_back({p + ".num_batches_tracked", {}});
+  };
+  v.push_back({"conv1.weight", {64, 3, 7, 7}});
+  bn("bn1", 64);
+  int inplanes = 64;
+  for (int li = 1; li <= 4; ++li) {
+    const int planes = 64 << (li - 1);
+    for (int bi = 0; bi < 2; ++bi) {
+      const std::string p = "layer" + std::to_string(li) + "." + std::to_string(bi);
+      const int cin = bi == 0 ? inplanes : planes;
+      v.push_back({p + ".conv1.weight", {planes, cin, 3, 3}});
+      bn(p + ".bn1", planes);
+      v.push_back({p + ".conv2.weight", {planes, planes, 3, 3}});
+      bn(p + ".bn2", planes);
+      if (bi == 0 && (li > 1)) {
+        v.push_back({p + ".downsample.0.weight", {planes, inplanes, 1, 1}});
+        bn(p + ".downsample.1", planes);
+      }
+    }
+    inplanes = planes;
+  }
+  const int up_out[3] = {256, 128, 64}, up_in[3] = {768, 384, 192};
+  for (int i = 0; i < 3; ++i) {
+    const std::string p = "conv_up_level" + std::to_string(i + 1);
+    v.push_back({p + ".weight", {up_out[i], up_in[i], 1, 1}});
+    v.push_back({p + ".bias", {up_out[i]}});
+  }
+  const auto order = sorted_heads(a);
+  for (int f = 0; f < 3; ++f)
+    for (int j : order) {
+      const std::string p = "fpn" + std::to_string(f) + "_" + a->head_names[j];
+      v.push_back({p + ".0.weight", {a->head_conv, kFpnC[f], 3, 3}});
+      v.push_back({p + ".0.bias", {a->head_conv}});
+      v.push_back({p + ".2.weight", {a->head_channels[j], a->head_conv, 1, 1}});
+      v.push_back({p + ".2.bias", {a->head_channels[j]}});
+    }
+  return v;
+}
+
+// ----------------------------------------------------------- packed layout
+struct PConv {
+  size_t w, b;
+  int N, K, Kpad;
+};
+struct PHeads {
+  size_t w3, b3, w1, b1;
+  int N, K;
+};
+struct Plan {
+  PConv stem;
+  PConv blk[4][2][2];  // [layer][block][conv1, conv2(+downsample)]
+  PConv fpn[3];
+  PHeads heads[3];
+  size_t total;
+};
+
+static Plan make_plan(const sfa_arch* a) {
+  Plan p;
+  size_t cur = 0;
+  auto take = [&](size_t n) {
+    const size_t o = cur;
+    cur = align_up(cur + n, 16);
+    return o;
+  };
+  auto conv = [&](int N, int K) {
+    PConv c;
+    c.N = N;
+    c.K = K;
+    c.Kpad = (int)align_up(K, 16);
+    c.w = take((size_t)N * c.Kpad);
+    c.b = take(N);
+    return c;
+  };
+  p.stem = conv(64, 49 * 4);
+  int inplanes = 64;
+  for (int li = 0; li < 4; ++li) {
+    const int planes = 64 << li;
+    for (int bi = 0; bi < 2; ++bi) {
+      const int cin = bi == 0 ? inplanes : planes;
+      const bool ds = bi == 0 && li > 0;
+      p.blk[li][bi][0] = conv(planes, 9 * cin);
+      p.blk[li][bi][1] = conv(planes, 9 * planes + (ds ? inplanes : 0));
+    }
+    inplanes = planes;
+  }
+  p.fpn[0] = conv(256, 768);
+  p.fpn[1] = conv(128, 384);
+  p.fpn[2] = conv(64, 192);
+  for (int f = 0; f < 3; ++f) {
+    PHeads& h = p.heads[f];
+    h.N = a->num_heads * a->head_conv;
+    h.K = 9 * kFpnC[f];
+    h.w3 = take((size_t)h.N * h.K);
+    h.b3 = take(h.N);
+    h.w1 = take((size_t)a->num_heads * 4 * 64);
+    h.b1 = take((size_t)a->num_heads * 4);
+  }
+  p.total = cur;
+  return p;
+}
+
+struct StateView {
+  std::map<std::string, std::pair<const float*, Entry>> m;
+  const float* get(const std::string& n) const {
+    auto it = m.find(n);
+    return it == m.end() ? nullptr : it->second.first;
+  }
+};
+
+// OIHW conv weight folded by BN scale into W[o][(kh*KW+kw)*Cpad + c] + k_off.
+static void put_conv(float* W, int Kpad, int k_off, const float* w, int O, int I, int KH, int KW,
+                     int Cpad, const std::vector<double>& scale) {
+  for (int o = 0; o < O; ++o)
+    for (int c = 0; c < I; ++c)
+      for (int kh = 0; kh < KH; ++kh)
+        for (int kw = 0; kw < KW; ++kw) {
+          const double v = w[((o * I + c) * KH + kh) * KW + kw];
+          W[(size_t)o * Kpad + k_off + (kh * KW + kw) * Cpad + c] = (float)(v * scale[o]);
+        }
+}
+
+static void bn_fold(const StateView& s, const std::string& p, int C, std::vector<double>& scale,
+                    std::vector<double>& shift) {
+  const float* g = s.get(p + ".weight");
+  const float* b = s.get(p + ".bias");
+  const float* mu = s.get(p + ".running_mean");
+  const float* var = s.get(p + ".running_var");
+  scale.assign(C, 1.0);
+  shift.assign(C, 0.0);
+  for (int c = 0; c < C; ++c) {
+    scale[c] = (double)g[c] / std::sqrt((double)var[c] + 1e-5);
+    shift[c] = (double)b[c] - (double)mu[c] * scale[c];
+  }
+}
+
+}  // namespace sfa
+
+using namespace sfa;
+
+struct sfa_model {
+  sfa_arch arch;
+  const float* w;
+  Plan plan;
+};
+
+extern "C" int sfa_abi_version(void) { return SFA_ABI_VERSION; }
+extern "C" const char* sfa_last_error_string(void) { return g_err.c_str(); }
+
+extern "C" int sfa_state_count(const sfa_arch* arch) {
+  if (check_arch(arch) != SFA_OK) return -1;
+  return (int)state_layout(arch).size();
+}
+
+extern "C" int sfa_state_entry(const sfa_arch* arch, int index, char* name, int name_len,
+                               int64_t* shape4, int* ndim) {
+  int rc = check_arch(arch);
+  if (rc != SFA_OK) return rc;
+  const auto v = state_layout(arch);
+  SFA_CHECK_ARG(index >= 0 && index < (int)v.size(), "state index %d out of range", index);
+  const Entry& e = v[index];
+  SFA_CHECK_ARG(name && name_len > (int)e.name.size(), "name buffer too small");
+  memcpy(name, e.name.c_str(), e.name.size() + 1);
+  for (int i = 0; i < 4; ++i) shape4[i] = i < (int)e.shape.size() ? e.shape[i] : 0;
+  *ndim = (int)e.shape.size();
+  return SFA_OK;
+}
+
+extern "C" size_t sfa_state_floats(const sfa_arch* arch) {
+  if (check_arch(arch) != SFA_OK) return 0;
+  size_t n = 0;
+  for (const auto& e : state_layout(arch))
+    if (e.name.find("num_batches_tracked") == std::string::npos) n += numel(e);
+  return n;
+}
+
+extern "C" size_t sfa_packed_floats(const sfa_arch* arch) {
+  if (check_arch(arch) != SFA_OK) return 0;
+  return make_plan(arch).total;
+}
+
+extern "C" int sfa_pack_weights(const sfa_arch* arch, const float* state, size_t state_floats,
+                                float* packed) {
+  int rc = check_arch(arch);
+  if (rc != SFA_OK) return rc;
+  SFA_CHECK_ARG(state && packed, "pack: null argument");
+  SFA_CHECK_ARG(state_floats == sfa_state_floats(arch), "pack: expected %zu state floats, got %zu",
+                sfa_state_floats(arch), state_floats);
+  StateView s;
+  size_t off = 0;
+  for (const auto& e : state_layout(arch)) {
+    if (e.name.find("num_batches_tracked") != std::string::npos) continue;
+    s.m[e.name] = {state + off, e};
+    off += numel(e);
+  }
+  const Plan p = make_plan(arch);
+  std::fill(packed, packed + p.total, 0.f);
+  std::vector<double> sc, sh, sc2, sh2;
+
+  // stem: conv1 + bn1, input channels padded 3 -> 4
+  bn_fold(s, "bn1", 64, sc, sh);
+  put_conv(packed + p.stem.w, p.stem.Kpad, 0, s.get("conv1.weight"), 64, 3, 7, 7, 4, sc);
+  for (int o = 0; o < 64; ++o) packed[p.stem.b + o] = (float)sh[o];
+
+  int inplanes = 64;
+  for (int li = 0; li < 4; ++li) {
+    const int planes = 64 << li;
+    for (int bi = 0; bi < 2; ++bi) {
+      const std::string pre = "layer" + std::to_string(li + 1) + "." + std::to_string(bi);
+      const int cin = bi == 0 ? inplanes : planes;
+      const PConv& c1 = p.blk[li][bi][0];
+      bn_fold(s, pre + ".bn1", planes, sc, sh);
+      put_conv(packed + c1.w, c1.Kpad, 0, s.get(pre + ".conv1.weight"), planes, cin, 3, 3, cin, sc);
+      for (int o = 0; o < planes; ++o) packed[c1.b + o] = (float)sh[o];
+      const PConv& c2 = p.blk[li][bi][1];
+      bn_fold(s, pre + ".bn2", planes, sc, sh);
+      put_conv(packed + c2.w, c2.Kpad, 0, s.get(pre + ".conv2.weight"), planes, planes, 3, 3, planes,
+               sc);
+      if (bi == 0 && li > 0) {
+        bn_fold(s, pre + ".downsample.1", planes, sc2, sh2);
+        put_conv(packed + c2.w, c2.Kpad, 9 * planes, s.get(pre + ".downsample.0.weight"), planes,
+                 inplanes, 1, 1, inplanes, sc2);
+        for (int o = 0; o < planes; ++o) packed[c2.b + o] = (float)(sh[o] + sh2[o]);
+      } else {
+        for (int o = 0; o < planes; ++o) packed[c2.b + o] = (float)sh[o];
+      }
+    }
+    inplanes = planes;
+  }
+  const int up_out[3] = {256, 128, 64}, up_in[3] = {768, 384, 192};
+  for (int i = 0; i < 3; ++i) {
+    const std::string pre = "conv_up_level" + std::to_string(i + 1);
+    std::vector<double> one(up_out[i], 1.0);
+    put_conv(packed + p.fpn[i].w, p.fpn[i].Kpad, 0, s.get(pre + ".weight"), up_out[i], up_in[i], 1,
+             1, up_in[i], one);
+    const float* b = s.get(pre + ".bias");
+    for (int o = 0; o < up_out[i]; ++o) packed[p.fpn[i].b + o] = b[o];
+  }
+  for (int f = 0; f < 3; ++f) {
+    const PHeads& hp = p.heads[f];
+    std::vector<double> one(arch->head_conv, 1.0);
+    for (int j = 0; j < arch->num_heads; ++j) {
+      const std::string pre = "fpn" + std::to_string(f) + "_" + arch->head_names[j];
+      put_conv(packed + hp.w3 + (size_t)j * 64 * hp.K, hp.K, 0, s.get(pre + ".0.weight"), 64,
+               kFpnC[f], 3, 3, kFpnC[f], one);
+      const float* b3 = s.get(pre + ".0.bias");
+      for (int o = 0; o < 64; ++o) packed[hp.b3 + j * 64 + o] = b3[o];
+      const float* w1 = s.get(pre + ".2.weight");
+      const float* b1 = s.get(pre + ".2.bias");
+      for (int c = 0; c < arch->head_channels[j]; ++c) {
+        for (int k = 0; k < 64; ++k) packed[hp.w1 + (j * 4 + c) * 64 + k] = w1[c * 64 + k];
+        packed[hp.b1 + j * 4 + c] = b1[c];
+      }
+    }
+  }
+  return SFA_OK;
+}
+
+extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device, sfa_model** out) {
+  int rc = check_arch(arch);
+  if (rc != SFA_OK) return rc;
+  SFA_CHECK_ARG(packed_device && out, "model_create: null argument");
+  sfa_model* m = new sfa_model;
+  m->arch = *arch;
+  m->w = packed_device;
+  m->plan = make_plan(arch);
+  *out = m;
+  return SFA_OK;
+}
+
+extern "C" void sfa_model_destroy(sfa_model* model) { delete model; }
+
+namespace sfa {
+
+// Activation buffers of one forward (NHWC f32), carved from the workspace.
+struct Bufs {
+  size_t xin, s0, p0, t[4], a[4], l[4], up1, c1, up2, c2, up3, up4, L0, L1, L2, total;
+};
+
+static Bufs plan_bufs(const sfa_arch* arch, int B, int H, int W) {
+  Bufs b;
+  size_t cur = 0;
+  auto take = [&](size_t floats) {
+    const size_t o = cur;
+    cur = align_up(cur + floats * 4, 256);
+    return o;
+  };
+  const size_t P2 = (size_t)(H / 2) * (W / 2), P4 = (size_t)(H / 4) * (W / 4);
+  b.xin = take((size_t)B * H * W * 4);
+  b.s0 = take((size_t)B * P2 * 64);
+  b.p0 = take((size_t)B * P4 * 64);
+  for (int li = 0; li < 4; ++li) {
+    const size_t px = (size_t)(H >> (li + 2)) * (W >> (li + 2));
+    const size_t n = (size_t)B * px * (64 << li);
+    b.t[li] = take(n);
+    b.a[li] = take(n);
+    b.l[li] = take(n);
+  }
+  const size_t P8 = (size_t)(H / 8) * (W / 8), P16 = (size_t)(H / 16) * (W / 16);
+  b.up1 = take((size_t)B * P16 * 512);
+  b.c1 = take((size_t)B * P16 * 256);
+  b.up2 = take((size_t)B * P8 * 256);
+  b.c2 = take((size_t)B * P8 * 128);
+  b.up3 = take((size_t)B * P4 * 128);
+  b.up4 = take((size_t)B * P4 * 64);
+  int nch = 0;
+  for (int j = 0; j < arch->num_heads; ++j) nch += arch->head_channels[j];
+  b.L0 = take((size_t)nch * B * P8);
+  b.L1 = take((size_t)nch * B * P4);
+  b.L2 = take((size_t)nch * B * P4);
+  b.total = cur;
+  return b;
+}
+
+static ConvSeg seg(const float* x, int H, int W, int C, int k, int stride, int pad) {
+  ConvSeg g;
+  g.x = x;
+  g.H = H;
+  g.W = W;
+  g.C = C;
+  g.logC = ilog2(C);
+  g.KH = g.KW = k;
+  g.stride = stride;
+  g.pad = pad;
+  g.taps = k * k;
+  return g;
+}
+
+static ConvArgs conv_args(const float* wbase, const PConv& pc, int B, int OH, int OW, float* y,
+                          const float* res, int relu) {
+  ConvArgs a;
+  memset(&a, 0, sizeof a);
+  a.nseg = 1;
+  a.Kpad = pc.Kpad;
+  a.w = wbase + pc.w;
+  a.bias = wbase + pc.b;
+  a.res = res;
+  a.y = y;
+  a.M = B * OH * OW;
+  a.N = pc.N;
+  a.OH = OH;
+  a.OW = OW;
+  a.relu = relu;
+  return a;
+}
+
+}  // namespace sfa
+
+extern "C" size_t sfa_forward_workspace_size(const sfa_model* m, int batch, int height, int width) {
+  if (!m || batch <= 0 || height <= 0 || width <= 0) return 0;
+  return plan_bufs(&m->arch, batch, height, width).total;
+}
+
+extern "C" int64_t sfa_forward_buffer_offset(const sfa_model* m, int batch, int height, int width,
+                                             int which) {
+  if (!m || batch <= 0 || height <= 0 || width <= 0) return -1;
+  const Bufs b = plan_bufs(&m->arch, batch, height, width);
+  switch (which) {
+    case SFA_BUF_LAYER1: return (int64_t)b.l[0];
+    case SFA_BUF_LAYER2: return (int64_t)b.l[1];
+    case SFA_BUF_LAYER3: return (int64_t)b.l[2];
+    case SFA_BUF_LAYER4: return (int64_t)b.l[3];
+    case SFA_BUF_UP_LEVEL2: return (int64_t)b.up2;
+    case SFA_BUF_UP_LEVEL3: return (int64_t)b.up3;
+    case SFA_BUF_UP_LEVEL4: return (int64_t)b.up4;
+    case SFA_BUF_HEADS_L0: return (int64_t)b.L0;
+    case SFA_BUF_HEADS_L1: return (int64_t)b.L1;
+    case SFA_BUF_HEADS_L2: return (int64_t)b.L2;
+    default: return -1;
+  }
+}
+
+#define SFA_RC(expr)            \
+  do {                          \
+    int rc_ = (expr);           \
+    if (rc_ != SFA_OK) return rc_; \
+  } while (0)
+
+extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layout, int B, int H,
+                                 int W, float* const* head_out, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
+  SFA_CHECK_ARG(m && x && head_out && workspace, "forward: null argument");
+  SFA_CHECK_ARG(B >= 1 && H >= 32 && W >= 32 && H % 32 == 0 && W % 32 == 0,
+                "forward: input (%d, 3, %d, %d) must have H, W multiples of 32", B, H, W);
+  SFA_CHECK_ARG(in_layout == SFA_IN_NCHW3 || in_layout == SFA_IN_NHWC4, "forward: bad layout");
+  SFA_CHECK_ARG((long long)B * H * W * 4 < (1ll << 31), "forward: input too large");
+  const Bufs bf = plan_bufs(&m->arch, B, H, W);
+  if (workspace_bytes < bf.total) {
+    set_error("forward: workspace %zu < required %zu bytes", workspace_bytes, bf.total);
+    return SFA_E_WORKSPACE;
+  }
+  for (int j = 0; j < m->arch.num_heads; ++j) SFA_CHECK_ARG(head_out[j], "forward: null head out");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  char* ws = reinterpret_cast<char*>(workspace);
+  auto F = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
+  const float* wb = m->w;
+  const Plan& p = m->plan;
+
+  const float* xin = x;
+  if (in_layout == SFA_IN_NCHW3) {
+    SFA_RC(launch_nchw3_to_nhwc4(x, F(bf.xin), B, H, W, st));
+    xin = F(bf.xin);
+  }
+  const int H2 = H / 2, W2 = W / 2;
+  // stem conv7x7/s2/p3 + BN + ReLU   (fpn_resnet.py:179-181)
+  {
+    ConvArgs a = conv_args(wb, p.stem, B, H2, W2, F(bf.s0), nullptr, 1);
+    a.seg[0] = seg(xin, H, W, 4, 7, 2, 3);
+    SFA_RC(launch_conv(a, EPI_STD, st));
+  }
+  SFA_RC(launch_maxpool3s2(F(bf.s0), F(bf.p0), B, H2, W2, 64, st));  // :182
+  // residual layers (fpn_resnet.py:184-187)
+  const float* xcur = F(bf.p0);
+  int h = H / 4, w = W / 4, cin = 64;
+  for (int li = 0; li < 4; ++li) {
+    const int planes = 64 << li;
+    const int stride = li == 0 ? 1 : 2;
+    const int oh = h / stride, ow = w / stride;
+    float* t = F(bf.t[li]);
+    float* av = F(bf.a[li]);
+    float* lv = F(bf.l[li]);
+    // block 0: conv1 (stride) ; conv2 (+ fused 1x1/s2 downsample for li > 0)
+    {
+      ConvArgs a = conv_args(wb, p.blk[li][0][0], B, oh, ow, t, nullptr, 1);
+      a.seg[0] = seg(xcur, h, w, cin, 3, stride, 1);
+      SFA_RC(launch_conv(a, EPI_STD, st));
+    }
+    {
+      ConvArgs a = conv_args(wb, p.blk[li][0][1], B, oh, ow, av, li == 0 ? xcur : nullptr, 1);
+      a.seg[0] = seg(t, oh, ow, planes, 3, 1, 1);
+      if (li > 0) {
+        a.nseg = 2;
+        a.kseg1 = 9 * planes;
+        a.seg[1] = seg(xcur, h, w, cin, 1, stride, 0);
+      }
+      SFA_RC(launch_conv(a, EPI_STD, st));
+    }
+    // block 1
+    {
+      ConvArgs a = conv_args(wb, p.blk[li][1][0], B, oh, ow, t, nullptr, 1);
+      a.seg[0] = seg(av, oh, ow, planes, 3, 1, 1);
+      SFA_RC(launch_conv(a, EPI_STD, st));
+    }
+    {
+      ConvArgs a = conv_args(wb, p.blk[li][1][1], B, oh, ow, lv, av, 1);
+      a.seg[0] = seg(t, oh, ow, planes, 3, 1, 1);
+      SFA_RC(launch_conv(a, EPI_STD, st));
+    }
+    xcur = lv;
+    h = oh;
+    w = ow;
+    cin = planes;
+  }
+  // FPN top-down (fpn_resnet.py:197-210): bilinear x2 (align_corners) + channel
+  // concat, read by the 1x1 conv as two K-segments (no concat buffer).
+  const int H4 = H / 4, W4 = W / 4, H8 = H / 8, W8 = W / 8, H16 = H / 16, W16 = W / 16;
+  SFA_RC(launch_upsample2x(F(bf.l[3]), F(bf.up1), B, H / 32, W / 32, 512, st));
+  {
+    ConvArgs a = conv_args(wb, p.fpn[0], B, H16, W16, F(bf.c1), nullptr, 0);
+    a.nseg = 2;
+    a.kseg1 = 512;
+    a.seg[0] = seg(F(bf.up1), H16, W16, 512, 1, 1, 0);
+    a.seg[1] = seg(F(bf.l[2]), H16, W16, 256, 1, 1, 0);
+    SFA_RC(launch_conv(a, EPI_STD, st));
+  }
+  SFA_RC(launch_upsample2x(F(bf.c1), F(bf.up2), B, H16, W16, 256, st));
+  {
+    ConvArgs a = conv_args(wb, p.fpn[1], B, H8, W8, F(bf.c2), nullptr, 0);
+    a.nseg = 2;
+    a.kseg1 = 256;
+    a.seg[0] = seg(F(bf.up2), H8, W8, 256, 1, 1, 0);
+    a.seg[1] = seg(F(bf.l[1]), H8, W8, 128, 1, 1, 0);
+    SFA_RC(launch_conv(a, EPI_STD, st));
+  }
+  SFA_RC(launch_upsample2x(F(bf.c2), F(bf.up3), B, H8, W8, 128, st));
+  {
+    ConvArgs a = conv_args(wb, p.fpn[2], B, H4, W4, F(bf.up4), nullptr, 0);
+    a.nseg = 2;
+    a.kseg1 = 128;
+    a.seg[0] = seg(F(bf.up3), H4, W4, 128, 1, 1, 0);
+    a.seg[1] = seg(F(bf.l[0]), H4, W4, 64, 1, 1, 0);
+    SFA_RC(launch_conv(a, EPI_STD, st));
+  }
+  // Detection heads (fpn_resnet.py:219-233): per level all heads in one launch,
+  // conv3x3 -> ReLU -> conv1x1 fused; channel-planar level outputs.
+  int hoff[SFA_MAX_HEADS] = {0};
+  int nch = 0;
+  for (int j = 0; j < m->arch.num_heads; ++j) {
+    hoff[j] = nch;
+    nch += m->arch.head_channels[j];
+  }
+  const float* lin[3] = {F(bf.up2), F(bf.up3), F(bf.up4)};
+  const int lh[3] = {H8, H4, H4}, lw[3] = {W8, W4, W4};
+  float* lout[3] = {F(bf.L0), F(bf.L1), F(bf.L2)};
+  for (int f = 0; f < 3; ++f) {
+    const PHeads& hp = p.heads[f];
+    ConvArgs a;
+    memset(&a, 0, sizeof a);
+    a.nseg = 1;
+    a.seg[0] = seg(lin[f], lh[f], lw[f], kFpnC[f], 3, 1, 1);
+    a.Kpad = hp.K;
+    a.w = wb + hp.w3;
+    a.bias = wb + hp.b3;
+    a.M = B * lh[f] * lw[f];
+    a.N = hp.N;
+    a.OH = lh[f];
+    a.OW = lw[f];
+    a.relu = 1;
+    a.hw1 = wb + hp.w1;
+    a.hb1 = wb + hp.b1;
+    for (int j = 0; j < m->arch.num_heads; ++j) {
+      a.hch[j] = m->arch.head_channels[j];
+      a.hoff[j] = hoff[j];
+    }
+    a.hout = lout[f];
+    SFA_RC(launch_conv(a, EPI_HEAD, st));
+  }
+  // apply_kfpn (fpn_resnet.py:248-254)
+  KfpnOut ko;
+  memset(&ko, 0, sizeof ko);
+  for (int j = 0; j < m->arch.num_heads; ++j) {
+    ko.ptr[j] = head_out[j];
+    ko.ch[j] = m->arch.head_channels[j];
+    ko.off[j] = hoff[j];
+  }
+  ko.num_heads = m->arch.num_heads;
+  ko.total_ch = nch;
+  SFA_RC(launch_kfpn(F(bf.L0), F(bf.L1), F(bf.L2), ko, B, H4, W4, st));
+  return SFA_OK;
+}

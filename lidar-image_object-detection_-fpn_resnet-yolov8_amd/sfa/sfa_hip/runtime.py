@@ -1,0 +1,352 @@
+"""Host runtime over the C ABI: weight packing, engines, device buffers, streams.
+
+torch is used only as plumbing (device memory, the current HIP stream, graph
+capture); every computation on the hot path is a libsfa_hip kernel.
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import SfaNativeError, check, lib
+
+DEFAULT_HEADS = {"hm_cen": 3, "cen_offset": 2, "direction": 2, "z_coor": 1, "dim": 3}
+DEFAULT_BOUNDARY = {"minX": 0, "maxX": 50, "minY": -25, "maxY": 25, "minZ": -2.73, "maxZ": 1.27}
+
+
+def _require_gpu_tensor(t: torch.Tensor, what: str, dtype=torch.float32) -> torch.Tensor:
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise SfaNativeError(f"{what}: the HIP path needs a tensor on a GPU device "
+                             f"(got {getattr(t, 'device', type(t))}); there is no CPU fallback")
+    if t.dtype != dtype:
+        raise TypeError(f"{what}: expected {dtype}, got {t.dtype}")
+    return t.contiguous()
+
+
+def _boundary_arr(boundary: dict):
+    vals = [boundary[k] for k in ("minX", "maxX", "minY", "maxY", "minZ", "maxZ")]
+    return (ctypes.c_double * 6)(*[float(v) for v in vals])
+
+
+# ------------------------------------------------------------------ weights
+def pack_state_dict(state: dict, arch) -> np.ndarray:
+    """Reference-format state_dict (tensors or arrays) -> packed float32 host array."""
+    L = lib()
+    layout = _lib.state_layout(arch)
+    parts = []
+    for name, shape in layout:
+        if name.endswith("num_batches_tracked"):
+            continue
+        if name not in state:
+            raise KeyError(f"state_dict is missing {name}")
+        v = state[name]
+        v = v.detach().to("cpu", torch.float32).numpy() if isinstance(v, torch.Tensor) else np.asarray(
+            v, np.float32)
+        if tuple(v.shape) != tuple(shape):
+            raise ValueError(f"{name}: shape {tuple(v.shape)} != {tuple(shape)}")
+        parts.append(np.ascontiguousarray(v, np.float32).reshape(-1))
+    flat = np.concatenate(parts) if parts else np.zeros(0, np.float32)
+    nfl = L.sfa_state_floats(ctypes.byref(arch))
+    if flat.size != nfl:
+        raise ValueError(f"state has {flat.size} floats, expected {nfl}")
+    packed = np.zeros(L.sfa_packed_floats(ctypes.byref(arch)), np.float32)
+    check(L.sfa_pack_weights(ctypes.byref(arch), flat.ctypes.data, flat.size, packed.ctypes.data),
+          "sfa_pack_weights")
+    return packed
+
+
+class KfpnEngine:
+    """A device copy of the packed weights + an sfa_model handle + workspace cache."""
+
+    def __init__(self, arch, packed_host: np.ndarray, device):
+        self.arch = arch
+        self.device = torch.device(device)
+        self.heads = [(arch.head_names[j].value.decode(), int(arch.head_channels[j]))
+                      for j in range(arch.num_heads)]
+        self.weights = torch.from_numpy(packed_host).to(self.device)
+        h = ctypes.c_void_p()
+        check(lib().sfa_model_create(ctypes.byref(arch), self.weights.data_ptr(), ctypes.byref(h)),
+              "sfa_model_create")
+        self._h = h
+        self._ws = {}
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None) is not None and self._h.value:
+                lib().sfa_model_destroy(self._h)
+        except Exception:
+            pass
+
+    def workspace_bytes(self, B, H, W) -> int:
+        return int(lib().sfa_forward_workspace_size(self._h, B, H, W))
+
+    def workspace(self, B, H, W) -> torch.Tensor:
+        key = (B, H, W)
+        ws = self._ws.get(key)
+        if ws is None:
+            ws = torch.empty(self.workspace_bytes(B, H, W), dtype=torch.uint8, device=self.device)
+            self._ws = {key: ws}  # keep only the latest shape resident
+        return ws
+
+    def alloc_outputs(self, B, H, W):
+        return {name: torch.empty((B, ch, H // 4, W // 4), dtype=torch.float32, device=self.device)
+                for name, ch in self.heads}
+
+    def forward_into(self, x: torch.Tensor, outs: dict, in_layout: int = _lib.IN_NCHW3,
+                     workspace: torch.Tensor = None, stream: int = None) -> dict:
+        if in_layout == _lib.IN_NCHW3:
+            B, C, H, W = x.shape
+            if C != 3:
+                raise ValueError(f"expected (B, 3, H, W) input, got {tuple(x.shape)}")
+        else:
+            B, H, W, C = x.shape
+            if C != 4:
+                raise ValueError(f"expected (B, H, W, 4) input, got {tuple(x.shape)}")
+        ws = workspace if workspace is not None else self.workspace(B, H, W)
+        ptrs = (ctypes.c_void_p * len(self.heads))(*[outs[n].data_ptr() for n, _ in self.heads])
+        check(lib().sfa_model_forward(self._h, x.data_ptr(), in_layout, B, H, W, ptrs, ws.data_ptr(),
+                                      ws.numel(), stream if stream is not None else
+                                      _lib.stream_ptr(self.device)), "sfa_model_forward")
+        return outs
+
+    def debug_views(self, ws: torch.Tensor, B, H, W) -> dict:
+        """NCHW views of intermediate maps left in the workspace by the last forward."""
+        L = lib()
+
+        def nhwc(which, h, w, c):
+            off = int(L.sfa_forward_buffer_offset(self._h, B, H, W, which))
+            t = ws[off: off + B * h * w * c * 4].view(torch.float32).view(B, h, w, c)
+            return t.permute(0, 3, 1, 2)
+
+        v = {f"layer{i + 1}": nhwc(i, H >> (i + 2), W >> (i + 2), 64 << i) for i in range(4)}
+        v["up_level2"] = nhwc(4, H // 8, W // 8, 256)
+        v["up_level3"] = nhwc(5, H // 4, W // 4, 128)
+        v["up_level4"] = nhwc(6, H // 4, W // 4, 64)
+        nch = sum(c for _, c in self.heads)
+        lv = []
+        for k, (h, w) in enumerate(((H // 8, W // 8), (H // 4, W // 4), (H // 4, W // 4))):
+            off = int(L.sfa_forward_buffer_offset(self._h, B, H, W, 7 + k))
+            lv.append(ws[off: off + nch * B * h * w * 4].view(torch.float32).view(nch, B, h, w))
+        levels, c0 = {}, 0
+        for name, ch in self.heads:
+            levels[name] = [t[c0:c0 + ch].permute(1, 0, 2, 3) for t in lv]
+            c0 += ch
+        v["levels"] = levels
+        return v
+
+    def forward(self, x: torch.Tensor, in_layout: int = _lib.IN_NCHW3) -> dict:
+        x = _require_gpu_tensor(x, "PoseResNet.forward")
+        if in_layout == _lib.IN_NCHW3:
+            B, _, H, W = x.shape
+        else:
+            B, H, W, _ = x.shape
+        if H % 32 or W % 32:
+            raise ValueError(f"input H, W must be multiples of 32, got {H}x{W}")
+        with torch.cuda.device(self.device):
+            outs = self.alloc_outputs(B, H, W)
+            return self.forward_into(x, outs, in_layout)
+
+
+# --------------------------------------------------------------------- BEV
+class BevVoxelizer:
+    """sfa_bev_voxelize with its (self-cleaning) scratch kept resident."""
+
+    def __init__(self, device, max_batch: int = 16):
+        self.device = torch.device(device)
+        self.max_batch = 0
+        self.scratch = None
+        self._grow(max_batch)
+
+    def _grow(self, b):
+        if b <= self.max_batch:
+            return
+        if b > _lib.SFA_BEV_MAX_BATCH:
+            raise ValueError(f"BEV batch {b} > {_lib.SFA_BEV_MAX_BATCH}")
+        self.scratch = torch.zeros(int(lib().sfa_bev_scratch_size(b)), dtype=torch.uint8,
+                                   device=self.device)
+        self.max_batch = b
+
+    def __call__(self, points: torch.Tensor, offsets, boundary=DEFAULT_BOUNDARY,
+                 layout: int = _lib.BEV_NHWC4_F32, flags: int = _lib.BEV_RAW, out=None,
+                 stream: int = None) -> torch.Tensor:
+        points = _require_gpu_tensor(points, "makeBEVMap")
+        if points.ndim != 2 or points.shape[1] != 4:
+            raise ValueError(f"points must be (N, 4), got {tuple(points.shape)}")
+        offs = np.asarray(offsets, dtype=np.int64)
+        B = offs.size - 1
+        if B < 1 or offs[-1] > points.shape[0] or offs[0] < 0 or np.any(np.diff(offs) < 0):
+            raise ValueError("bad frame offsets")
+        self._grow(B)
+        if out is None:
+            if layout == _lib.BEV_NHWC4_F32:
+                out = torch.empty((B, 608, 608, 4), dtype=torch.float32, device=self.device)
+            else:
+                dt = torch.float64 if layout == _lib.BEV_NCHW3_F64 else torch.float32
+                out = torch.empty((B, 3, 608, 608), dtype=dt, device=self.device)
+        offs_c = (ctypes.c_int64 * (B + 1))(*offs.tolist())
+        check(lib().sfa_bev_voxelize(points.data_ptr() if points.numel() else None, offs_c, B,
+                                     _boundary_arr(boundary), flags, layout, out.data_ptr(),
+                                     self.scratch.data_ptr(),
+                                     stream if stream is not None else _lib.stream_ptr(self.device)),
+              "sfa_bev_voxelize")
+        return out
+
+
+_voxelizers = {}
+
+
+def voxelizer(device) -> BevVoxelizer:
+    device = torch.device(device)
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    v = _voxelizers.get(device)
+    if v is None:
+        v = _voxelizers[device] = BevVoxelizer(device)
+    return v
+
+
+def filter_points(points: torch.Tensor, boundary=DEFAULT_BOUNDARY) -> torch.Tensor:
+    """get_filtered_lidar on the device: (N, 4) f32 -> (M, 4) f32 (order kept, z -= minZ)."""
+    points = _require_gpu_tensor(points, "get_filtered_lidar")
+    n = points.shape[0]
+    out = torch.empty((max(n, 1), 4), dtype=torch.float32, device=points.device)
+    cnt = torch.zeros(1, dtype=torch.int64, device=points.device)
+    scratch = torch.empty(int(lib().sfa_filter_scratch_size(n)), dtype=torch.uint8,
+                          device=points.device)
+    check(lib().sfa_filter_points(points.data_ptr() if n else None, n, _boundary_arr(boundary),
+                                  out.data_ptr(), cnt.data_ptr(), scratch.data_ptr(), scratch.numel(),
+                                  _lib.stream_ptr(points.device)), "sfa_filter_points")
+    m = int(cnt.item())
+    return out[:m]
+
+
+# ------------------------------------------------------------------ decode
+def sigmoid_clamp_(x: torch.Tensor) -> torch.Tensor:
+    if x.device.type != "cuda" or not x.is_contiguous() or x.dtype != torch.float32:
+        raise SfaNativeError("_sigmoid: the HIP path needs a contiguous float32 GPU tensor")
+    check(lib().sfa_sigmoid_clamp_inplace(x.data_ptr(), x.numel(), _lib.stream_ptr(x.device)),
+          "sfa_sigmoid_clamp_inplace")
+    return x
+
+
+class Decoder:
+    """sfa_decode with a cached workspace."""
+
+    def __init__(self):
+        self._ws = {}
+
+    def workspace(self, device, B, C, K):
+        key = (str(device), B, C, K)
+        ws = self._ws.get(key)
+        if ws is None:
+            ws = torch.empty(int(lib().sfa_decode_workspace_size(B, C, K)), dtype=torch.uint8,
+                             device=device)
+            self._ws[key] = ws
+        return ws
+
+    def __call__(self, hm, off, dirn, z, dim, K=40, apply_sigmoid=False, out=None,
+                 stream: int = None):
+        hm = _require_gpu_tensor(hm, "decode")
+        dirn, z, dim = (_require_gpu_tensor(t, "decode") for t in (dirn, z, dim))
+        if off is not None:
+            off = _require_gpu_tensor(off, "decode")
+        B, C, H, W = hm.shape
+        for t, c in ((off, 2), (dirn, 2), (z, 1), (dim, 3)):
+            if t is not None and tuple(t.shape) != (B, c, H, W):
+                raise ValueError(f"decode: map shape {tuple(t.shape)} != {(B, c, H, W)}")
+        if out is None:
+            out = torch.empty((B, K, 10), dtype=torch.float32, device=hm.device)
+        ws = self.workspace(hm.device, B, C, K)
+        check(lib().sfa_decode(hm.data_ptr(), off.data_ptr() if off is not None else None,
+                               dirn.data_ptr(), z.data_ptr(), dim.data_ptr(), B, C, H, W, int(K),
+                               1 if apply_sigmoid else 0, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                               stream if stream is not None else _lib.stream_ptr(hm.device)),
+              "sfa_decode")
+        return out
+
+
+_decoder = Decoder()
+
+
+def decode(hm, off, dirn, z, dim, K=40, apply_sigmoid=False):
+    return _decoder(hm, off, dirn, z, dim, K=K, apply_sigmoid=apply_sigmoid)
+
+
+# ---------------------------------------------------------------- pipeline
+class DetectorPipeline:
+    """Fixed-shape hot path on one GPU: [points ->] BEV -> KFPN forward -> decode.
+
+    All buffers are allocated once; ``run()`` only enqueues kernels on the current
+    stream, so it can be captured in a HIP graph (``capture()``).
+    """
+
+    def __init__(self, engine: KfpnEngine, batch: int, height: int = 608, width: int = 608,
+                 K: int = 50, with_bev: bool = False, max_points: int = 0):
+        self.engine = engine
+        self.dev = engine.device
+        self.B, self.H, self.W, self.K = batch, height, width, K
+        self.with_bev = with_bev
+        with torch.cuda.device(self.dev):
+            self.ws = engine.workspace(batch, height, width)
+            self.outs = engine.alloc_outputs(batch, height, width)
+            self.dets = torch.empty((batch, K, 10), dtype=torch.float32, device=self.dev)
+            self.dec_ws = _decoder.workspace(self.dev, batch, dict(engine.heads)["hm_cen"], K)
+            if with_bev:
+                if (height, width) != (608, 608):
+                    raise ValueError("the BEV grid is 608x608 (config/kitti_config.py:45-46)")
+                self.vox = BevVoxelizer(self.dev, batch)
+                self.bev = torch.empty((batch, 608, 608, 4), dtype=torch.float32, device=self.dev)
+                self.points = torch.zeros((max(max_points, 1), 4), dtype=torch.float32,
+                                          device=self.dev)
+                self.offsets = np.zeros(batch + 1, np.int64)
+            else:
+                self.x = torch.empty((batch, 3, height, width), dtype=torch.float32, device=self.dev)
+        self.graph = None
+
+    def set_points(self, clouds):
+        """Copy a list of (N_i, 4) float32 clouds into the resident point buffer."""
+        offs = np.zeros(len(clouds) + 1, np.int64)
+        for i, c in enumerate(clouds):
+            offs[i + 1] = offs[i] + c.shape[0]
+        if len(clouds) != self.B or offs[-1] > self.points.shape[0]:
+            raise ValueError("clouds do not fit the pipeline's point buffer")
+        host = torch.from_numpy(np.concatenate(clouds).astype(np.float32))
+        self.points[: offs[-1]].copy_(host)
+        self.offsets = offs
+
+    def run(self):
+        st = _lib.stream_ptr(self.dev)
+        if self.with_bev:
+            self.vox(self.points, self.offsets, layout=_lib.BEV_NHWC4_F32, flags=_lib.BEV_RAW,
+                     out=self.bev, stream=st)
+            self.engine.forward_into(self.bev, self.outs, _lib.IN_NHWC4, self.ws, st)
+        else:
+            self.engine.forward_into(self.x, self.outs, _lib.IN_NCHW3, self.ws, st)
+        o = self.outs
+        _decoder(o["hm_cen"], o["cen_offset"], o["direction"], o["z_coor"], o["dim"], K=self.K,
+                 apply_sigmoid=True, out=self.dets, stream=st)
+        return self.dets
+
+    def capture(self):
+        """Capture run() into a HIP graph (launch-overhead amortisation)."""
+        with torch.cuda.device(self.dev):
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self.run()  # warm (module load, lazy init) outside capture
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.run()
+            self.graph = g
+        return g
+
+    def replay(self):
+        if self.graph is None:
+            return self.run()
+        self.graph.replay()
+        return self.dets

@@ -1,0 +1,105 @@
+"""GPU parity of BEV voxelisation + point filter vs the reference fixtures (bit-exact)."""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+import golden_cases as gc
+from oracle import bev_oracle
+from sfa_hip import _lib, runtime
+
+pytestmark = pytest.mark.gpu
+
+NAMES = ["sweep_s1", "sweep_s2_sub", "kat_edges", "single_point", "empty_after_filter"]
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_make_bev_map_f64_bit_exact(golden, gpu, name):
+    from data_process.kitti_bev_utils import makeBEVMap
+    from data_process.kitti_data_utils import get_filtered_lidar
+    g = golden.bev
+    cloud = dict(gc.bev_cases(g))[name]
+    filt = get_filtered_lidar(cloud, gc.BOUNDARY)  # HIP compaction
+    assert filt.shape[0] == int(g[f"{name}/filtered_n"])
+    assert _sha(filt) == str(g[f"{name}/filtered_sha"])
+    bev = makeBEVMap(filt, gc.BOUNDARY)  # HIP voxeliser, f64 like the reference
+    assert bev.dtype == np.float64 and bev.shape == (3, 608, 608)
+    assert _sha(bev) == str(g[f"{name}/map_sha"])
+
+
+def test_raw_batch_layouts_bit_exact(golden, gpu):
+    """Fused filter+voxelise on a ragged batch, all three output layouts."""
+    g = golden.bev
+    clouds = [c for _, c in gc.bev_cases(g)]
+    offs = np.cumsum([0] + [c.shape[0] for c in clouds])
+    pts = torch.from_numpy(np.concatenate(clouds)).to(gpu)
+    vox = runtime.BevVoxelizer(gpu, len(clouds))
+    f64 = vox(pts, offs, gc.BOUNDARY, layout=_lib.BEV_NCHW3_F64).cpu().numpy()
+    f32 = vox(pts, offs, gc.BOUNDARY, layout=_lib.BEV_NCHW3_F32).cpu().numpy()
+    nhwc = vox(pts, offs, gc.BOUNDARY, layout=_lib.BEV_NHWC4_F32).cpu().numpy()
+    for b, name in enumerate(NAMES):
+        assert _sha(f64[b]) == str(g[f"{name}/map_sha"]), name
+        np.testing.assert_array_equal(f32[b], f64[b].astype(np.float32))
+        np.testing.assert_array_equal(nhwc[b][..., :3].transpose(2, 0, 1), f32[b])
+        assert np.all(nhwc[b][..., 3] == 0)
+
+
+def test_scratch_stays_clean_and_repeatable(gpu):
+    from sfa_hip import synthetic
+    clouds = [synthetic.synthetic_point_cloud(s) for s in (3, 4)]
+    offs = np.cumsum([0] + [c.shape[0] for c in clouds])
+    pts = torch.from_numpy(np.concatenate(clouds)).to(gpu)
+    vox = runtime.BevVoxelizer(gpu, 2)
+    a = vox(pts, offs, gc.BOUNDARY, layout=_lib.BEV_NCHW3_F64).cpu().numpy()
+    assert int(vox.scratch.count_nonzero()) == 0
+    b = vox(pts, offs, gc.BOUNDARY, layout=_lib.BEV_NCHW3_F64).cpu().numpy()
+    np.testing.assert_array_equal(a, b)
+    for i, c in enumerate(clouds):
+        exp = bev_oracle.makeBEVMap(bev_oracle.get_filtered_lidar(c, gc.BOUNDARY), gc.BOUNDARY)
+        np.testing.assert_array_equal(a[i], exp)
+
+
+def test_shuffled_ties_follow_input_order(gpu):
+    """Equal max-z points in a cell: the FIRST in input order supplies intensity."""
+    rng = np.random.default_rng(5)
+    n = 20000
+    pts = np.zeros((n, 4), np.float32)
+    pts[:, 0] = rng.uniform(10, 10.3, n)
+    pts[:, 1] = rng.uniform(-0.3, 0.3, n)
+    pts[:, 2] = rng.choice(np.float32([-1.0, 0.5]), n)
+    pts[:, 3] = rng.uniform(0, 1, n)
+    exp = bev_oracle.makeBEVMap(bev_oracle.get_filtered_lidar(pts, gc.BOUNDARY), gc.BOUNDARY)
+    got = runtime.BevVoxelizer(gpu, 1)(torch.from_numpy(pts).to(gpu), [0, n], gc.BOUNDARY,
+                                       layout=_lib.BEV_NCHW3_F64).cpu().numpy()[0]
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_back_boundary_wraps_like_numpy(gpu):
+    """boundary_back: rows never shifted by minX -> negative numpy indices wrap."""
+    from sfa_hip import synthetic
+    back = {"minX": -50, "maxX": 0, "minY": -25, "maxY": 25, "minZ": -2.73, "maxZ": 1.27}
+    c = synthetic.synthetic_point_cloud(6)
+    filt = bev_oracle.get_filtered_lidar(c, back)
+    exp = bev_oracle.makeBEVMap(filt, back)
+    got = runtime.BevVoxelizer(gpu, 1)(torch.from_numpy(c).to(gpu), [0, c.shape[0]], back,
+                                       layout=_lib.BEV_NCHW3_F64).cpu().numpy()[0]
+    np.testing.assert_array_equal(got, exp)
+
+
+def test_filter_large_random(gpu):
+    rng = np.random.default_rng(9)
+    n = 1_000_003
+    pts = rng.uniform(-60, 60, (n, 4)).astype(np.float32)
+    pts[:, 2] = rng.uniform(-4, 3, n)
+    got = runtime.filter_points(torch.from_numpy(pts).to(gpu), gc.BOUNDARY).cpu().numpy()
+    np.testing.assert_array_equal(got, bev_oracle.get_filtered_lidar(pts, gc.BOUNDARY))
+
+
+def test_cpu_input_refused():
+    with pytest.raises(_lib.SfaNativeError):
+        runtime.filter_points(torch.zeros(4, 4), gc.BOUNDARY)
