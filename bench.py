@@ -163,16 +163,17 @@ def main():
     rank, world, dev = init_dist(args.gpus)
     pipe = build_pipeline(dev, args, rank)
     steps = StepGraphs(pipe, not args.no_graph)
-    gathered = None
-    if world > 1:
+    gather = world > 1
+    if gather:
         import torch.distributed as dist
-        gathered = torch.empty((world,) + tuple(pipe.dets.shape), dtype=torch.float32, device=dev)
+        from sfa_hip import dist as sdist
+        frame_ids = torch.arange(rank * args.batch, (rank + 1) * args.batch, device=dev)
 
     def one_step():
         steps.run(0)
         steps.run(1)
-        if gathered is not None:
-            dist.all_gather_into_tensor(gathered, pipe.dets)
+        if gather:
+            sdist.gather_detections(pipe.dets, frame_ids)
 
     for _ in range(args.warmup):
         one_step()
@@ -189,8 +190,8 @@ def main():
         ev[k][1].record(stream)
         steps.run(1)
         ev[k][2].record(stream)
-        if gathered is not None:
-            dist.all_gather_into_tensor(gathered, pipe.dets)
+        if gather:
+            sdist.gather_detections(pipe.dets, frame_ids)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
