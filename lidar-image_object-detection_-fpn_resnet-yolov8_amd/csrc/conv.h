@@ -13,7 +13,37 @@ struct ConvSeg {
   int H, W, C, logC;   // C is a power of two (4 .. 512)
   int KH, KW, stride, pad;
   int taps;            // KH * KW
+  int kdiv_mul, kdiv_sh;  // tap / KW == (tap * kdiv_mul) >> kdiv_sh for tap < 64
+  unsigned bytes;      // size of x in bytes (< 2^31): buffer-load range, OOB -> 0
 };
+
+// Fills a segment; returns false if the tensor is too large for 32-bit offsets.
+inline bool make_seg(ConvSeg& g, const float* x, int B, int H, int W, int C, int k, int stride, int pad) {
+  g.x = x;
+  g.H = H;
+  g.W = W;
+  g.C = C;
+  g.logC = ilog2(C);
+  g.KH = g.KW = k;
+  g.stride = stride;
+  g.pad = pad;
+  g.taps = k * k;
+  g.kdiv_mul = 1;
+  g.kdiv_sh = 0;
+  for (int sh = 0; sh < 16 && k > 1; ++sh) {
+    const int mul = ((1 << sh) + k - 1) / k;
+    bool ok = true;
+    for (int t = 0; t < 64 && ok; ++t) ok = ((t * mul) >> sh) == t / k;
+    if (ok) {
+      g.kdiv_mul = mul;
+      g.kdiv_sh = sh;
+      break;
+    }
+  }
+  const unsigned long long bytes = (unsigned long long)B * H * W * C * 4ull;
+  g.bytes = (unsigned)bytes;
+  return bytes < (1ull << 31);
+}
 
 enum ConvEpilogue { EPI_STD = 0, EPI_HEAD = 1 };
 

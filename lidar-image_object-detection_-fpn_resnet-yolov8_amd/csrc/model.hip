@@ -390,17 +390,9 @@ static Bufs plan_bufs(const sfa_arch* arch, int B, int H, int W) {
   return b;
 }
 
-static ConvSeg seg(const float* x, int H, int W, int C, int k, int stride, int pad) {
+static ConvSeg seg(const float* x, int B, int H, int W, int C, int k, int stride, int pad) {
   ConvSeg g;
-  g.x = x;
-  g.H = H;
-  g.W = W;
-  g.C = C;
-  g.logC = ilog2(C);
-  g.KH = g.KW = k;
-  g.stride = stride;
-  g.pad = pad;
-  g.taps = k * k;
+  make_seg(g, x, B, H, W, C, k, stride, pad);  // oversize inputs are rejected by launch_conv
   return g;
 }
 
@@ -483,7 +475,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   // stem conv7x7/s2/p3 + BN + ReLU   (fpn_resnet.py:179-181)
   {
     ConvArgs a = conv_args(wb, p.stem, B, H2, W2, F(bf.s0), nullptr, 1);
-    a.seg[0] = seg(xin, H, W, 4, 7, 2, 3);
+    a.seg[0] = seg(xin, B, H, W, 4, 7, 2, 3);
     SFA_RC(launch_conv(a, EPI_STD, st));
   }
   SFA_RC(launch_maxpool3s2(F(bf.s0), F(bf.p0), B, H2, W2, 64, st));  // :182
@@ -500,28 +492,28 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     // block 0: conv1 (stride) ; conv2 (+ fused 1x1/s2 downsample for li > 0)
     {
       ConvArgs a = conv_args(wb, p.blk[li][0][0], B, oh, ow, t, nullptr, 1);
-      a.seg[0] = seg(xcur, h, w, cin, 3, stride, 1);
+      a.seg[0] = seg(xcur, B, h, w, cin, 3, stride, 1);
       SFA_RC(launch_conv(a, EPI_STD, st));
     }
     {
       ConvArgs a = conv_args(wb, p.blk[li][0][1], B, oh, ow, av, li == 0 ? xcur : nullptr, 1);
-      a.seg[0] = seg(t, oh, ow, planes, 3, 1, 1);
+      a.seg[0] = seg(t, B, oh, ow, planes, 3, 1, 1);
       if (li > 0) {
         a.nseg = 2;
         a.kseg1 = 9 * planes;
-        a.seg[1] = seg(xcur, h, w, cin, 1, stride, 0);
+        a.seg[1] = seg(xcur, B, h, w, cin, 1, stride, 0);
       }
       SFA_RC(launch_conv(a, EPI_STD, st));
     }
     // block 1
     {
       ConvArgs a = conv_args(wb, p.blk[li][1][0], B, oh, ow, t, nullptr, 1);
-      a.seg[0] = seg(av, oh, ow, planes, 3, 1, 1);
+      a.seg[0] = seg(av, B, oh, ow, planes, 3, 1, 1);
       SFA_RC(launch_conv(a, EPI_STD, st));
     }
     {
       ConvArgs a = conv_args(wb, p.blk[li][1][1], B, oh, ow, lv, av, 1);
-      a.seg[0] = seg(t, oh, ow, planes, 3, 1, 1);
+      a.seg[0] = seg(t, B, oh, ow, planes, 3, 1, 1);
       SFA_RC(launch_conv(a, EPI_STD, st));
     }
     xcur = lv;
@@ -537,8 +529,8 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     ConvArgs a = conv_args(wb, p.fpn[0], B, H16, W16, F(bf.c1), nullptr, 0);
     a.nseg = 2;
     a.kseg1 = 512;
-    a.seg[0] = seg(F(bf.up1), H16, W16, 512, 1, 1, 0);
-    a.seg[1] = seg(F(bf.l[2]), H16, W16, 256, 1, 1, 0);
+    a.seg[0] = seg(F(bf.up1), B, H16, W16, 512, 1, 1, 0);
+    a.seg[1] = seg(F(bf.l[2]), B, H16, W16, 256, 1, 1, 0);
     SFA_RC(launch_conv(a, EPI_STD, st));
   }
   SFA_RC(launch_upsample2x(F(bf.c1), F(bf.up2), B, H16, W16, 256, st));
@@ -546,8 +538,8 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     ConvArgs a = conv_args(wb, p.fpn[1], B, H8, W8, F(bf.c2), nullptr, 0);
     a.nseg = 2;
     a.kseg1 = 256;
-    a.seg[0] = seg(F(bf.up2), H8, W8, 256, 1, 1, 0);
-    a.seg[1] = seg(F(bf.l[1]), H8, W8, 128, 1, 1, 0);
+    a.seg[0] = seg(F(bf.up2), B, H8, W8, 256, 1, 1, 0);
+    a.seg[1] = seg(F(bf.l[1]), B, H8, W8, 128, 1, 1, 0);
     SFA_RC(launch_conv(a, EPI_STD, st));
   }
   SFA_RC(launch_upsample2x(F(bf.c2), F(bf.up3), B, H8, W8, 128, st));
@@ -555,8 +547,8 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     ConvArgs a = conv_args(wb, p.fpn[2], B, H4, W4, F(bf.up4), nullptr, 0);
     a.nseg = 2;
     a.kseg1 = 128;
-    a.seg[0] = seg(F(bf.up3), H4, W4, 128, 1, 1, 0);
-    a.seg[1] = seg(F(bf.l[0]), H4, W4, 64, 1, 1, 0);
+    a.seg[0] = seg(F(bf.up3), B, H4, W4, 128, 1, 1, 0);
+    a.seg[1] = seg(F(bf.l[0]), B, H4, W4, 64, 1, 1, 0);
     SFA_RC(launch_conv(a, EPI_STD, st));
   }
   // Detection heads (fpn_resnet.py:219-233): per level all heads in one launch,
@@ -575,7 +567,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     ConvArgs a;
     memset(&a, 0, sizeof a);
     a.nseg = 1;
-    a.seg[0] = seg(lin[f], lh[f], lw[f], kFpnC[f], 3, 1, 1);
+    a.seg[0] = seg(lin[f], B, lh[f], lw[f], kFpnC[f], 3, 1, 1);
     a.Kpad = hp.K;
     a.w = wb + hp.w3;
     a.bias = wb + hp.b3;

@@ -1,0 +1,217 @@
+// Micro-benchmark of conv_mfma_kernel tile configurations on the KFPN layer
+// shapes at bs=16, 608x608 (tools only; not part of the product library).
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/convbench.hip -o tools/convbench
+//   ./tools/convbench [iters]
+// Every candidate's output is compared with the first candidate's (same math,
+// different tiling -> differences only from summation order).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_kernel.h"
+
+namespace sfa {
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vfprintf(stderr, fmt, ap);
+  va_end(ap);
+  fprintf(stderr, "\n");
+}
+}  // namespace sfa
+
+using namespace sfa;
+
+#define CK(x)                                                               \
+  do {                                                                      \
+    hipError_t e = (x);                                                     \
+    if (e != hipSuccess) {                                                  \
+      fprintf(stderr, "%s: %s (%s:%d)\n", #x, hipGetErrorString(e), __FILE__, __LINE__); \
+      exit(1);                                                              \
+    }                                                                       \
+  } while (0)
+
+static float* dev_random(size_t n, unsigned seed, float scale) {
+  std::vector<float> h(n);
+  unsigned s = seed * 2654435761u + 12345u;
+  for (size_t i = 0; i < n; ++i) {
+    s = s * 1664525u + 1013904223u;
+    h[i] = scale * ((float)(s >> 8) / 16777216.0f - 0.5f);
+  }
+  float* d;
+  CK(hipMalloc(&d, n * 4));
+  CK(hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice));
+  return d;
+}
+
+struct Shape {
+  const char* name;
+  int B, H, W, C, k, stride, pad, N;
+  bool head, res;
+};
+
+typedef std::function<int(const ConvArgs&, hipStream_t)> Launch;
+struct Cand {
+  std::string name;
+  int BK;
+  Launch fn;
+};
+
+#define CAND(BM, BN, WM, WN, BK, EPI, OCC)                                              \
+  Cand {                                                                                \
+    #BM "x" #BN " w" #WM "x" #WN " bk" #BK " occ" #OCC, BK,                              \
+        [](const ConvArgs& a, hipStream_t s) { return launch_conv_cfg<BM, BN, WM, WN, BK, EPI, OCC>(a, s); } \
+  }
+
+int main(int argc, char** argv) {
+  const int iters = argc > 1 ? atoi(argv[1]) : 20;
+  const char* only = argc > 2 ? argv[2] : nullptr;
+  std::vector<Shape> shapes = {
+      {"stem 7x7/2 4->64", 16, 608, 608, 4, 7, 2, 3, 64, false, false},
+      {"layer1 3x3 64->64 +res", 16, 152, 152, 64, 3, 1, 1, 64, false, true},
+      {"layer2 3x3 128->128", 16, 76, 76, 128, 3, 1, 1, 128, false, false},
+      {"layer3 3x3 256->256", 16, 38, 38, 256, 3, 1, 1, 256, false, false},
+      {"layer4 3x3 512->512", 16, 19, 19, 512, 3, 1, 1, 512, false, false},
+      {"head L1 3x3 128->5x64", 16, 152, 152, 128, 3, 1, 1, 320, true, false},
+      {"head L2 3x3 64->5x64", 16, 152, 152, 64, 3, 1, 1, 320, true, false},
+      {"head L0 3x3 256->5x64", 16, 76, 76, 256, 3, 1, 1, 320, true, false},
+  };
+  std::vector<Cand> n64 = {
+      CAND(128, 64, 32, 64, 16, EPI_STD, 3), CAND(128, 64, 32, 64, 16, EPI_STD, 4),
+      CAND(128, 64, 32, 64, 16, EPI_STD, 5), CAND(64, 64, 32, 32, 16, EPI_STD, 4),
+      CAND(64, 64, 32, 32, 16, EPI_STD, 6), CAND(64, 64, 32, 32, 32, EPI_STD, 4),
+      CAND(128, 64, 32, 64, 32, EPI_STD, 3),
+  };
+  std::vector<Cand> nbig = {
+      CAND(64, 64, 32, 32, 16, EPI_STD, 4), CAND(64, 64, 32, 32, 16, EPI_STD, 6),
+      CAND(64, 64, 32, 32, 32, EPI_STD, 3), CAND(64, 64, 32, 32, 32, EPI_STD, 4),
+      CAND(64, 128, 32, 64, 16, EPI_STD, 3), CAND(64, 128, 32, 64, 16, EPI_STD, 4),
+      CAND(128, 128, 64, 64, 16, EPI_STD, 3), CAND(64, 128, 32, 64, 32, EPI_STD, 3),
+  };
+  std::vector<Cand> heads = {
+      CAND(128, 64, 32, 64, 16, EPI_HEAD, 3), CAND(128, 64, 32, 64, 16, EPI_HEAD, 4),
+      CAND(128, 64, 32, 64, 16, EPI_HEAD, 5), CAND(64, 64, 32, 32, 16, EPI_HEAD, 4),
+      CAND(64, 64, 32, 32, 16, EPI_HEAD, 6), CAND(64, 64, 32, 32, 32, EPI_HEAD, 4),
+      CAND(128, 64, 32, 64, 32, EPI_HEAD, 3),
+  };
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (const Shape& sh : shapes) {
+    if (only && !strstr(sh.name, only)) continue;
+    const int OH = (sh.H + 2 * sh.pad - sh.k) / sh.stride + 1;
+    const int OW = (sh.W + 2 * sh.pad - sh.k) / sh.stride + 1;
+    const int M = sh.B * OH * OW;
+    const int K = sh.k * sh.k * sh.C;
+    const int Kpad = (K + 31) / 32 * 32;
+    float* x = dev_random((size_t)sh.B * sh.H * sh.W * sh.C, 1, 1.0f);
+    float* w = dev_random((size_t)sh.N * Kpad, 2, 2.0f / std::sqrt((float)K));
+    float* b = dev_random(sh.N, 3, 0.2f);
+    float* res = sh.res ? dev_random((size_t)M * sh.N, 4, 1.0f) : nullptr;
+    float* hw1 = dev_random(8 * 4 * 64, 5, 0.25f);
+    float* hb1 = dev_random(8 * 4, 6, 0.2f);
+    const int nh = sh.N / 64;
+    const size_t ysz = sh.head ? (size_t)11 * M : (size_t)M * sh.N;
+    float *y, *y0;
+    CK(hipMalloc(&y, ysz * 4));
+    CK(hipMalloc(&y0, ysz * 4));
+    // zero weight columns beyond K so Kpad=224/208 variants agree
+    {
+      std::vector<float> hwv((size_t)sh.N * Kpad);
+      CK(hipMemcpy(hwv.data(), w, hwv.size() * 4, hipMemcpyDeviceToHost));
+      for (int n = 0; n < sh.N; ++n)
+        for (int k = K; k < Kpad; ++k) hwv[(size_t)n * Kpad + k] = 0.f;
+      CK(hipMemcpy(w, hwv.data(), hwv.size() * 4, hipMemcpyHostToDevice));
+    }
+    ConvArgs a;
+    memset(&a, 0, sizeof a);
+    a.nseg = 1;
+    make_seg(a.seg[0], x, sh.B, sh.H, sh.W, sh.C, sh.k, sh.stride, sh.pad);
+    a.w = w;
+    a.bias = b;
+    a.res = res;
+    a.M = M;
+    a.N = sh.N;
+    a.OH = OH;
+    a.OW = OW;
+    a.relu = 1;
+    a.hw1 = hw1;
+    a.hb1 = hb1;
+    int off = 0;
+    const int hc[5] = {3, 2, 2, 1, 3};
+    for (int j = 0; j < nh; ++j) {
+      a.hch[j] = hc[j % 5];
+      a.hoff[j] = off;
+      off += a.hch[j];
+    }
+    const double flop = 2.0 * M * sh.N * (double)K;
+    std::vector<Cand>& cands = sh.head ? heads : (sh.N == 64 ? n64 : nbig);
+    printf("\n== %s  M=%d N=%d K=%d  (%.2f GFLOP)\n", sh.name, M, sh.N, K, flop / 1e9);
+    std::vector<float> ref, got;
+    for (size_t ci = 0; ci < cands.size(); ++ci) {
+      Cand& c = cands[ci];
+      a.Kpad = c.BK == 16 ? (K + 15) / 16 * 16 : Kpad;
+      // weights are [N][Kpad]; re-stride when Kpad differs from the allocation
+      float* wv = w;
+      if (a.Kpad != Kpad) {
+        std::vector<float> hwv((size_t)sh.N * Kpad), hw2((size_t)sh.N * a.Kpad);
+        CK(hipMemcpy(hwv.data(), w, hwv.size() * 4, hipMemcpyDeviceToHost));
+        for (int n = 0; n < sh.N; ++n)
+          for (int k = 0; k < a.Kpad; ++k) hw2[(size_t)n * a.Kpad + k] = hwv[(size_t)n * Kpad + k];
+        CK(hipMalloc(&wv, hw2.size() * 4));
+        CK(hipMemcpy(wv, hw2.data(), hw2.size() * 4, hipMemcpyHostToDevice));
+      }
+      a.w = wv;
+      a.y = y;
+      a.hout = y;
+      CK(hipMemset(y, 0, ysz * 4));
+      if (c.fn(a, st) != SFA_OK) {
+        printf("  %-32s unsupported\n", c.name.c_str());
+        continue;
+      }
+      CK(hipStreamSynchronize(st));
+      got.resize(ysz);
+      CK(hipMemcpy(got.data(), y, ysz * 4, hipMemcpyDeviceToHost));
+      double maxd = 0, maxr = 0;
+      if (ci == 0) {
+        ref = got;
+      } else {
+        for (size_t i = 0; i < ysz; ++i) {
+          maxd = std::max(maxd, (double)std::fabs(got[i] - ref[i]));
+          maxr = std::max(maxr, (double)std::fabs(ref[i]));
+        }
+      }
+      std::vector<float> ms;
+      for (int it = 0; it < iters; ++it) {
+        CK(hipEventRecord(e0, st));
+        c.fn(a, st);
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float t;
+        CK(hipEventElapsedTime(&t, e0, e1));
+        ms.push_back(t);
+      }
+      std::sort(ms.begin(), ms.end());
+      const float med = ms[ms.size() / 2];
+      printf("  %-32s %9.1f us  %7.1f TF/s  maxdiff %.2e (|ref| %.2e)\n", c.name.c_str(), med * 1e3,
+             flop / (med * 1e-3) / 1e12, maxd, maxr);
+      if (wv != w) CK(hipFree(wv));
+    }
+    CK(hipFree(x));
+    CK(hipFree(w));
+    CK(hipFree(b));
+    if (res) CK(hipFree(res));
+    CK(hipFree(hw1));
+    CK(hipFree(hb1));
+    CK(hipFree(y));
+    CK(hipFree(y0));
+  }
+  return 0;
+}
