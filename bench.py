@@ -129,6 +129,20 @@ class StepGraphs:
             self.graphs[i].replay()
 
 
+def traffic_per_forward(args):
+    """HBM bytes of the conv launches of one forward, from the committed PMC pass
+    (tools/pmc_forward.sh -> profiles/*_pmc_forward.json; rocprofv3 cannot run inside
+    this process). Only reported for the configuration it was measured on."""
+    if args.workload != "bev_infer" or args.batch != 16:
+        return None
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_forward.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        return int(json.load(f)["conv_hbm_bytes_per_forward"])
+
+
 def cpu_baseline(args):
     """The oracle (torch fp32 CPU restatement of the reference forward + numpy decode),
     on a bounded sample of the same workload (the reference Python cannot travel)."""
@@ -242,7 +256,7 @@ def main():
                 "peak": PEAK_FP32_MFMA_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
-                "traffic": None,
+                "traffic": traffic_per_forward(args),
                 "algorithmic_flop_per_step": flop_step,
             },
         }

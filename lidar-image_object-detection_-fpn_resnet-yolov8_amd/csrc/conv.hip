@@ -31,20 +31,21 @@ int launch_conv(const ConvArgs& a, int epilogue, hipStream_t st) {
   }
   // Tile choice per shape, from tools/convbench.hip sweeps on MI355X (round 1):
   // 32x64 / 32x32 wave tiles at 4 waves per SIMD hide the gather latency best;
-  // BK = 32 pays only for the long-K, few-block layer4 shapes.
+  // BK = 32 pays only for the long-K, few-block layer4 shapes; the LDS-DMA ring
+  // (GLDS) gains 2-8 % on the heads and layer3, nothing elsewhere.
   if (epilogue == EPI_HEAD) {
     if (a.N / 64 > SFA_MAX_HEADS) {
       set_error("conv: too many heads");
       return SFA_E_UNSUPPORTED;
     }
-    return launch_conv_cfg<128, 64, 32, 64, 16, EPI_HEAD, 4>(a, st);
+    return launch_conv_cfg<128, 64, 32, 64, 16, EPI_HEAD, 4, true>(a, st);
   }
   if (a.N == 64) return launch_conv_cfg<128, 64, 32, 64, 16, EPI_STD, 4>(a, st);
   if (a.N % 128 == 0) {
     if ((long long)ceil_div(a.M, 128) * (a.N / 128) >= 512)
       return launch_conv_cfg<128, 128, 64, 64, 16, EPI_STD, 3>(a, st);
     if ((long long)ceil_div(a.M, 64) * (a.N / 128) >= 512)
-      return launch_conv_cfg<64, 128, 32, 64, 16, EPI_STD, 4>(a, st);
+      return launch_conv_cfg<64, 128, 32, 64, 16, EPI_STD, 4, true>(a, st);
     if (a.Kpad % 32 == 0 && (a.nseg == 1 || a.kseg1 % 32 == 0))
       return launch_conv_cfg<64, 64, 32, 32, 32, EPI_STD, 4>(a, st);
   }

@@ -24,9 +24,16 @@ namespace sfa {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-template <int BM, int BN, int WM, int WN, int BK, int EPI, int OCC>
+// GLDS: stage the A/B tiles with buffer_load ... lds (LDS-DMA, no VGPR staging)
+//   into a 3-deep ring of unpadded, XOR-swizzled tiles (BK = 16 only).
+// ABL: diagnostic ablation bits for tools/convbench (0 in the product):
+//   1 = no global loads in the K loop, 2 = no barrier, 4 = no LDS fragment reads.
+template <int BM, int BN, int WM, int WN, int BK, int EPI, int OCC, bool GLDS = false, int ABL = 0>
 __global__ void __launch_bounds__(256, OCC) conv_mfma_kernel(const ConvArgs a) {
-  constexpr int LDK = BK + 4;
+  static_assert(!GLDS || BK == 16, "the LDS-DMA ring is built for BK = 16");
+  // GLDS rows are 64 B, quad q of row R stored at position q ^ ((R >> 2) & 3)
+  constexpr int LDK = GLDS ? BK : BK + 4;
+  constexpr int NSTAGE = GLDS ? 3 : 2;
   constexpr int WAVES_N = BN / WN;
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves per block");
   static_assert(BK == 16 || BK == 32, "BK");
@@ -40,8 +47,9 @@ __global__ void __launch_bounds__(256, OCC) conv_mfma_kernel(const ConvArgs a) {
   constexpr int STAGE = (BM + BN) * LDK;
   constexpr int HCH = BM < 128 ? BM : 128;  // head epilogue row chunk
   constexpr int HEAD_LDS = EPI == EPI_HEAD ? HCH * 65 : 0;
-  constexpr int LDS_FLOATS = (2 * STAGE > HEAD_LDS) ? 2 * STAGE : HEAD_LDS;
+  constexpr int LDS_FLOATS = (NSTAGE * STAGE > HEAD_LDS) ? NSTAGE * STAGE : HEAD_LDS;
   __shared__ __attribute__((aligned(16))) float smem[LDS_FLOATS];
+  float* lds_stage = smem;  // GLDS: destination stage of the next load_tile
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
@@ -56,7 +64,11 @@ __global__ void __launch_bounds__(256, OCC) conv_mfma_kernel(const ConvArgs a) {
   // tap offset is added.  Addresses are 32-bit byte offsets into a buffer
   // resource: an out-of-window tap gets an offset past the end and the hardware
   // returns zeros (the conv's zero padding) — no branch, no 64-bit math.
-  const int kq = tid % QPR, rr = tid / QPR;
+  // register mode: thread loads quad kq of row rr (+RPP*i); GLDS mode: lane l of wave
+  // w fills row (w + 4i)*16 + (l >> 2) -- the same rows -- at LDS quad l & 3, which
+  // holds logical quad (l & 3) ^ ((l >> 4) & 3)
+  const int kq = GLDS ? ((lane & 3) ^ ((lane >> 4) & 3)) : tid % QPR;
+  const int rr = tid / QPR;
   constexpr int NSEG = 2;
   int r_ih[NSEG][A_LD], r_iw[NSEG][A_LD], r_pix[NSEG][A_LD];
 #pragma unroll
@@ -99,10 +111,17 @@ __global__ void __launch_bounds__(256, OCC) conv_mfma_kernel(const ConvArgs a) {
     const int toff = kh * g.W + kw;
 #pragma unroll
     for (int i = 0; i < A_LD; ++i) {
-      const bool ok = tap_ok && (unsigned)(r_ih[sg][i] + kh) < (unsigned)g.H &&
-                      (unsigned)(r_iw[sg][i] + kw) < (unsigned)g.W;
+      // bitwise '&' (not '&&'): keeps this a select instead of divergent branches
+      const bool ok = tap_ok & ((unsigned)(r_ih[sg][i] + kh) < (unsigned)g.H) &
+                      ((unsigned)(r_iw[sg][i] + kw) < (unsigned)g.W);
       const unsigned off = ok ? (unsigned)((((r_pix[sg][i] + toff) << g.logC) + c) << 2) : 0x80000000u;
-      ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      if constexpr (GLDS) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(lds_stage + (wave + 4 * i) * 16 * BK), 16,
+            off, 0, 0, 0);
+      } else {
+        ra[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+      }
     }
   };
   auto load_tile = [&](int kt) {
@@ -114,7 +133,13 @@ __global__ void __launch_bounds__(256, OCC) conv_mfma_kernel(const ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < B_LD; ++j) {
       const unsigned off = (unsigned)(((n0 + rr + RPP * j) * a.Kpad + k0 + 4 * kq) << 2);
-      rb[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsw, off, 0, 0));
+      if constexpr (GLDS) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsw, (__attribute__((address_space(3))) void*)(lds_stage + (BM + (wave + 4 * j) * 16) * BK),
+            16, off, 0, 0, 0);
+      } else {
+        rb[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsw, off, 0, 0));
+      }
     }
   };
   auto store_tile = [&](int stage) {
@@ -138,20 +163,24 @@ __global__ void __launch_bounds__(256, OCC) conv_mfma_kernel(const ConvArgs a) {
 
   const int r = lane & 31, h = lane >> 5;
   auto compute = [&](int stage) {
-    const float* As = smem + stage * STAGE;
+    const float* As = smem + (ABL & 4 ? 0 : stage * STAGE);
     const float* Bs = As + BM * LDK;
     f32x4 af[TM][FR], bf[TN][FR];
+    // row R = 32-row group base + r; with GLDS, (R >> 2) & 3 == (r >> 2) & 3
+    const int sw = GLDS ? ((r >> 2) & 3) : 0;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
-      const float* p = As + (wm * WM + mi * 32 + r) * LDK + KS * h;
+      const float* p = As + (wm * WM + mi * 32 + r) * LDK;
 #pragma unroll
-      for (int f = 0; f < FR; ++f) af[mi][f] = *reinterpret_cast<const f32x4*>(p + 4 * f);
+      for (int f = 0; f < FR; ++f)
+        af[mi][f] = *reinterpret_cast<const f32x4*>(p + 4 * ((KS / 4 * h + f) ^ sw));
     }
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
-      const float* p = Bs + (wn * WN + ni * 32 + r) * LDK + KS * h;
+      const float* p = Bs + (wn * WN + ni * 32 + r) * LDK;
 #pragma unroll
-      for (int f = 0; f < FR; ++f) bf[ni][f] = *reinterpret_cast<const f32x4*>(p + 4 * f);
+      for (int f = 0; f < FR; ++f)
+        bf[ni][f] = *reinterpret_cast<const f32x4*>(p + 4 * ((KS / 4 * h + f) ^ sw));
     }
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
@@ -168,6 +197,23 @@ __global__ void __launch_bounds__(256, OCC) conv_mfma_kernel(const ConvArgs a) {
   };
 
   const int nk = a.Kpad / BK;
+  if constexpr (GLDS) {
+    // 3-deep LDS-DMA ring: tiles kt+1 and kt+2 stream in while kt is consumed.
+    constexpr int L = A_LD + B_LD;  // DMA instructions per wave per tile
+    lds_stage = smem;
+    load_tile(0);
+    lds_stage = smem + STAGE;
+    load_tile(nk > 1 ? 1 : 0);
+    for (int kt = 0; kt < nk; ++kt) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(L) : "memory");  // tile kt landed (this wave)
+      __builtin_amdgcn_s_barrier();                              // ... and for every wave
+      lds_stage = smem + ((kt + 2) % 3) * STAGE;                 // read last in iteration kt-1
+      load_tile(kt + 2 < nk ? kt + 2 : nk - 1);
+      compute(kt % 3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  } else {
   load_tile(0);
   store_tile(0);
   __syncthreads();
@@ -176,10 +222,11 @@ __global__ void __launch_bounds__(256, OCC) conv_mfma_kernel(const ConvArgs a) {
     // Unconditional prefetch (the last iteration re-stages the final tile into the
     // idle buffer): keeps ra/rb in registers — a conditional definition made hipcc
     // spill them to scratch.
-    load_tile(kt + 1 < nk ? kt + 1 : kt);
+    if constexpr (!(ABL & 1)) load_tile(kt + 1 < nk ? kt + 1 : kt);
     compute(cur);
     store_tile(cur ^ 1);
-    __syncthreads();
+    if constexpr (!(ABL & 2)) __syncthreads();
+  }
   }
 
   if constexpr (EPI == EPI_STD) {
@@ -244,7 +291,7 @@ __global__ void __launch_bounds__(256, OCC) conv_mfma_kernel(const ConvArgs a) {
   }
 }
 
-template <int BM, int BN, int WM, int WN, int BK, int EPI, int OCC>
+template <int BM, int BN, int WM, int WN, int BK, int EPI, int OCC, bool GLDS = false, int ABL = 0>
 inline int launch_conv_cfg(const ConvArgs& a, hipStream_t st) {
   if (a.Kpad % BK != 0 || (a.nseg == 2 && a.kseg1 % BK != 0) || a.N % BN != 0) {
     set_error("conv: K/N not aligned to the tile (Kpad=%d kseg1=%d N=%d, BK=%d BN=%d)", a.Kpad,
@@ -258,7 +305,7 @@ inline int launch_conv_cfg(const ConvArgs& a, hipStream_t st) {
     set_error("conv: bad grid (M=%d N=%d)", a.M, a.N);
     return SFA_E_INVALID;
   }
-  hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, WN, BK, EPI, OCC>), dim3((unsigned)nblocks),
+  hipLaunchKernelGGL((conv_mfma_kernel<BM, BN, WM, WN, BK, EPI, OCC, GLDS, ABL>), dim3((unsigned)nblocks),
                      dim3(256), 0, st, a);
   SFA_LAUNCH_CHECK();
   return SFA_OK;

@@ -76,9 +76,21 @@ __global__ void __launch_bounds__(kDecThreads) decode_class_topk_kernel(
   const int bc = blockIdx.x;  // frame * C + class
   const float* src = hm + (size_t)bc * HW;
   const int tid = threadIdx.x;
-  for (int i = tid; i < HW; i += kDecThreads) {
-    const float v = src[i];
-    heat[i] = apply_sigmoid ? sigmoid_clamp_f(v) : v;
+  {
+    // all loads in flight before the first use (the map is read once; a strided
+    // load-use loop would pay one HBM/L2 latency per iteration)
+    constexpr int NL = kDecMaxHW / kDecThreads;
+    float v[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int i = tid + j * kDecThreads;
+      v[j] = i < HW ? __builtin_nontemporal_load(src + i) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int i = tid + j * kDecThreads;
+      if (i < HW) heat[i] = apply_sigmoid ? sigmoid_clamp_f(v[j]) : v[j];
+    }
   }
   __syncthreads();
   // 3x3 peak test (F.max_pool2d(3, 1, 1) pads with -inf); threads own contiguous
@@ -87,12 +99,12 @@ __global__ void __launch_bounds__(kDecThreads) decode_class_topk_kernel(
   const int i0 = tid * ipt;
   const int i1 = min(i0 + ipt, HW);
   float pk[(kDecMaxHW + kDecThreads - 1) / kDecThreads];
+  int y = i0 / W, x = i0 - (i0 / W) * W;  // walked incrementally (no per-item division)
 #pragma unroll
   for (int j = 0; j < (kDecMaxHW + kDecThreads - 1) / kDecThreads; ++j) {
     const int i = i0 + j;
     float out = 0.f;
     if (i < i1) {
-      const int y = i / W, x = i - y * W;
       const float v = heat[i];
       float m = v;
       for (int dy = -1; dy <= 1; ++dy) {
@@ -105,6 +117,10 @@ __global__ void __launch_bounds__(kDecThreads) decode_class_topk_kernel(
         }
       }
       out = (m == v) ? v : v * 0.f;  // heat * keep: non-peaks become (signed) zero
+      if (++x == W) {
+        x = 0;
+        ++y;
+      }
     }
     pk[j] = out;
   }
@@ -121,10 +137,22 @@ __global__ void __launch_bounds__(kDecThreads) decode_class_topk_kernel(
     const int shift = 24 - 8 * pass;
     for (int i = tid; i < 256; i += kDecThreads) hist[i] = 0u;
     __syncthreads();
+    // Non-peaks are exactly 0 (most of the map): count them per thread and add
+    // them with one atomic per wave instead of hammering a single LDS bin.
+    constexpr unsigned kZero = 0x80000000u;  // fkey(0.f)
+    unsigned nzero = 0;
     for (int i = i0; i < i1; ++i) {
       const unsigned k = fkey(heat[i]);
-      if ((k & pmask) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+      if ((k & pmask) == prefix) {
+        if (k == kZero)
+          ++nzero;
+        else
+          atomicAdd(&hist[(k >> shift) & 255u], 1u);
+      }
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nzero += __shfl_xor(nzero, o, 64);
+    if ((tid & 63) == 0 && nzero) atomicAdd(&hist[(kZero >> shift) & 255u], nzero);
     __syncthreads();
     if (tid < 64) {
       // descending suffix counts over 256 bins: lane handles bins 255-4*lane-3 .. 255-4*lane
@@ -196,16 +224,19 @@ __global__ void __launch_bounds__(256) decode_merge_gather_kernel(
     const unsigned* __restrict__ cand_key, const int* __restrict__ cand_idx, int C, int K, int H,
     int W, int apply_sigmoid, const float* __restrict__ off, const float* __restrict__ dir,
     const float* __restrict__ z, const float* __restrict__ dim, float* __restrict__ dets) {
+  __shared__ unsigned skey[16 * kDecMaxK];
   const int b = blockIdx.x;
   const int CK = C * K;
   const int HW = H * W;
   const unsigned* ck = cand_key + (size_t)b * CK;
   const int* ci = cand_idx + (size_t)b * CK;
+  for (int t = threadIdx.x; t < CK; t += blockDim.x) skey[t] = ck[t];
+  __syncthreads();
   for (int t = threadIdx.x; t < CK; t += blockDim.x) {
-    const unsigned k = ck[t];
+    const unsigned k = skey[t];
     int rank = 0;
     for (int j = 0; j < CK; ++j) {
-      const unsigned kj = ck[j];
+      const unsigned kj = skey[j];
       rank += (kj > k) || (kj == k && j < t);
     }
     if (rank >= K) continue;

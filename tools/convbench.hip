@@ -62,11 +62,13 @@ struct Cand {
   Launch fn;
 };
 
-#define CAND(BM, BN, WM, WN, BK, EPI, OCC)                                              \
+#define CANDG(BM, BN, WM, WN, BK, EPI, OCC, G, ABL)                                     \
   Cand {                                                                                \
-    #BM "x" #BN " w" #WM "x" #WN " bk" #BK " occ" #OCC, BK,                              \
-        [](const ConvArgs& a, hipStream_t s) { return launch_conv_cfg<BM, BN, WM, WN, BK, EPI, OCC>(a, s); } \
+    #BM "x" #BN " w" #WM "x" #WN " bk" #BK " occ" #OCC " glds" #G " abl" #ABL, BK,        \
+        [](const ConvArgs& a, hipStream_t s) { return launch_conv_cfg<BM, BN, WM, WN, BK, EPI, OCC, G, ABL>(a, s); } \
   }
+#define CANDA(BM, BN, WM, WN, BK, EPI, OCC, ABL) CANDG(BM, BN, WM, WN, BK, EPI, OCC, false, ABL)
+#define CAND(BM, BN, WM, WN, BK, EPI, OCC) CANDA(BM, BN, WM, WN, BK, EPI, OCC, 0)
 
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 20;
@@ -82,22 +84,19 @@ int main(int argc, char** argv) {
       {"head L0 3x3 256->5x64", 16, 76, 76, 256, 3, 1, 1, 320, true, false},
   };
   std::vector<Cand> n64 = {
-      CAND(128, 64, 32, 64, 16, EPI_STD, 3), CAND(128, 64, 32, 64, 16, EPI_STD, 4),
-      CAND(128, 64, 32, 64, 16, EPI_STD, 5), CAND(64, 64, 32, 32, 16, EPI_STD, 4),
-      CAND(64, 64, 32, 32, 16, EPI_STD, 6), CAND(64, 64, 32, 32, 32, EPI_STD, 4),
-      CAND(128, 64, 32, 64, 32, EPI_STD, 3),
+      CAND(128, 64, 32, 64, 16, EPI_STD, 4), CANDG(128, 64, 32, 64, 16, EPI_STD, 4, true, 0),
+      CANDG(128, 64, 32, 64, 16, EPI_STD, 3, true, 0), CANDG(256, 64, 64, 64, 16, EPI_STD, 2, true, 0),
+      CANDG(64, 64, 32, 32, 16, EPI_STD, 4, true, 0),
   };
   std::vector<Cand> nbig = {
-      CAND(64, 64, 32, 32, 16, EPI_STD, 4), CAND(64, 64, 32, 32, 16, EPI_STD, 6),
-      CAND(64, 64, 32, 32, 32, EPI_STD, 3), CAND(64, 64, 32, 32, 32, EPI_STD, 4),
-      CAND(64, 128, 32, 64, 16, EPI_STD, 3), CAND(64, 128, 32, 64, 16, EPI_STD, 4),
-      CAND(128, 128, 64, 64, 16, EPI_STD, 3), CAND(64, 128, 32, 64, 32, EPI_STD, 3),
+      CAND(64, 128, 32, 64, 16, EPI_STD, 4), CANDG(64, 128, 32, 64, 16, EPI_STD, 4, true, 0),
+      CANDG(128, 128, 64, 64, 16, EPI_STD, 2, true, 0), CANDG(64, 64, 32, 32, 16, EPI_STD, 4, true, 0),
+      CAND(64, 64, 32, 32, 32, EPI_STD, 4),
   };
   std::vector<Cand> heads = {
-      CAND(128, 64, 32, 64, 16, EPI_HEAD, 3), CAND(128, 64, 32, 64, 16, EPI_HEAD, 4),
-      CAND(128, 64, 32, 64, 16, EPI_HEAD, 5), CAND(64, 64, 32, 32, 16, EPI_HEAD, 4),
-      CAND(64, 64, 32, 32, 16, EPI_HEAD, 6), CAND(64, 64, 32, 32, 32, EPI_HEAD, 4),
-      CAND(128, 64, 32, 64, 32, EPI_HEAD, 3),
+      CAND(128, 64, 32, 64, 16, EPI_HEAD, 4), CANDG(128, 64, 32, 64, 16, EPI_HEAD, 4, true, 0),
+      CANDG(128, 64, 32, 64, 16, EPI_HEAD, 3, true, 0), CANDG(256, 64, 64, 64, 16, EPI_HEAD, 2, true, 0),
+      CANDG(64, 64, 32, 32, 16, EPI_HEAD, 4, true, 0),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
