@@ -61,10 +61,17 @@ def init_dist(n):
         raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # SFA_BENCH_SHARE_DEVICE=1 + SFA_DIST_BACKEND=gloo: rehearse the N>1 path on one GPU
+    if os.environ.get("SFA_BENCH_SHARE_DEVICE") == "1":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("SFA_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return rank, world, torch.device("cuda", local)
 
 
@@ -213,7 +220,8 @@ def main():
     fwd_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     if world > 1:
-        t = torch.tensor([elapsed, fwd_ms, dec_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, fwd_ms, dec_ms], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, fwd_ms, dec_ms = (float(v) for v in t.tolist())
     frames = world * args.batch * args.steps

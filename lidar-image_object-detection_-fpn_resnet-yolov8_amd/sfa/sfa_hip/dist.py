@@ -41,9 +41,12 @@ def gather_detections(dets: torch.Tensor, frame_ids: torch.Tensor, group=None):
     if dist.get_backend(group) == "nccl":
         dist.all_gather_into_tensor(out, dets.contiguous(), group=group)
         dist.all_gather_into_tensor(ids, frame_ids.contiguous(), group=group)
-    else:  # gloo (CPU tests)
-        dist.all_gather(list(out.chunk(world)), dets.contiguous(), group=group)
-        dist.all_gather(list(ids.chunk(world)), frame_ids.contiguous(), group=group)
+    else:  # gloo (CPU tests / single-GPU rehearsal): gather through host memory
+        oc, ic = out.cpu(), ids.cpu()
+        dist.all_gather(list(oc.chunk(world)), dets.contiguous().cpu(), group=group)
+        dist.all_gather(list(ic.chunk(world)), frame_ids.contiguous().cpu(), group=group)
+        out.copy_(oc)
+        ids.copy_(ic)
     return out, ids
 
 
