@@ -158,6 +158,46 @@ int sfa_decode(const float* hm, const float* off, const float* dir, const float*
                int apply_sigmoid, float* dets, void* workspace, size_t workspace_bytes,
                void* stream);
 
+/* ------------------------------------------------------------ fusion --
+ * Camera-LiDAR late fusion + NMS.  Replaces test6.py:310-348
+ * create_fused_detections_wrapper -> :231-308 bayesian_inspired_fuse_overlapping_detections
+ * (mode SFA_FUSE_BAYES) or test5.py:285-321 create_fused_detections -> :213-282
+ * fuse_overlapping_detections (SFA_FUSE_WEIGHTED), then test6.py:104-126
+ * apply_nms_to_fused_detections, all with test6.py:76-101 calculate_iou.
+ *
+ * Per frame b (CSR by DEVICE int32 offsets [batch+1]): YOLO boxes int32 [x,y,w,h],
+ * f64 confidence, int32 class id; SFA 2D boxes int32 [x,y,w,h], f64 confidence.
+ * At most 512 boxes per side per frame (a larger frame gets out_count = -1).
+ * Output for frame b starts at element yolo_offsets[b] + sfa_offsets[b] (capacity
+ * = its yolo + sfa count): the fused list in the reference's order (fused/kept YOLO
+ * entries in YOLO order, then unmatched SFA), source SFA_SRC_*, class id (SFA: 0);
+ * out_origin (optional) = index of the entry in its frame's INPUT list (YOLO for
+ * YOLO/fused entries, SFA for SFA entries), out_match (optional) = the SFA input
+ * index fused into a fused entry, else -1;
+ * out_keep = indices into that list of the NMS survivors, in NMS output order.
+ * All f64 arithmetic is IEEE without contraction: bit-identical to the Python. */
+enum sfa_fuse_mode { SFA_FUSE_BAYES = 0, SFA_FUSE_WEIGHTED = 1 };
+enum sfa_fuse_source { SFA_SRC_YOLO = 0, SFA_SRC_LIDAR = 1, SFA_FUSED = 2 };
+typedef struct sfa_fusion_params {
+  double conf_threshold;        /* keep detections with conf >= this (default 0.3) */
+  double fusion_iou_threshold;  /* associate when IoU >= this (default 0.7) */
+  double nms_threshold;         /* suppress when IoU > this (default 0.5) */
+  int mode;                     /* SFA_FUSE_BAYES | SFA_FUSE_WEIGHTED */
+  int apply_nms;                /* 0: fusion only */
+} sfa_fusion_params;
+
+/* IoU matrix out[i][j] = calculate_iou(a[i], b[j]) (test6.py:76-101), f64. */
+int sfa_iou_matrix(const int32_t* boxes_a, int na, const int32_t* boxes_b, int nb, double* out,
+                   void* stream);
+
+int sfa_fuse_detections(int batch, const int32_t* yolo_boxes, const double* yolo_conf,
+                        const int32_t* yolo_cls, const int32_t* yolo_offsets,
+                        const int32_t* sfa_boxes, const double* sfa_conf,
+                        const int32_t* sfa_offsets, const sfa_fusion_params* params,
+                        int32_t* out_boxes, double* out_conf, int32_t* out_cls, int32_t* out_src,
+                        int32_t* out_origin, int32_t* out_match, int32_t* out_count,
+                        int32_t* out_keep, int32_t* out_keep_count, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -71,6 +71,19 @@ _PROTOS = {
     "sfa_decode": (_c_int, [_vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int,
                             _vp, _vp, _c_size, _vp]),
 }
+
+class SfaFusionParams(ctypes.Structure):
+    _fields_ = [("conf_threshold", ctypes.c_double), ("fusion_iou_threshold", ctypes.c_double),
+                ("nms_threshold", ctypes.c_double), ("mode", ctypes.c_int),
+                ("apply_nms", ctypes.c_int)]
+
+
+FUSE_BAYES, FUSE_WEIGHTED = 0, 1
+SRC_YOLO, SRC_LIDAR, SRC_FUSED = 0, 1, 2
+_PROTOS["sfa_iou_matrix"] = (_c_int, [_vp, _c_int, _vp, _c_int, _vp, _vp])
+_PROTOS["sfa_fuse_detections"] = (_c_int, [_c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                           ctypes.POINTER(SfaFusionParams), _vp, _vp, _vp, _vp,
+                                           _vp, _vp, _vp, _vp, _vp, _vp])
 EXPORTED_SYMBOLS = tuple(_PROTOS)
 
 _lib = None

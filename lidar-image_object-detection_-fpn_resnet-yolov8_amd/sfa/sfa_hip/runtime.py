@@ -350,3 +350,85 @@ class DetectorPipeline:
             return self.run()
         self.graph.replay()
         return self.dets
+
+
+# ------------------------------------------------------------------ fusion
+def iou_matrix(boxes_a, boxes_b, device=None) -> torch.Tensor:
+    """calculate_iou for every pair (test6.py:76-101): int [x, y, w, h] boxes -> (na, nb) f64."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    a = torch.as_tensor(np.asarray(boxes_a, np.int32).reshape(-1, 4)).to(dev)
+    b = torch.as_tensor(np.asarray(boxes_b, np.int32).reshape(-1, 4)).to(dev)
+    out = torch.empty((a.shape[0], b.shape[0]), dtype=torch.float64, device=dev)
+    check(lib().sfa_iou_matrix(a.data_ptr() if a.numel() else None, a.shape[0],
+                               b.data_ptr() if b.numel() else None, b.shape[0],
+                               out.data_ptr() if out.numel() else None, _lib.stream_ptr(dev)),
+          "sfa_iou_matrix")
+    return out
+
+
+class FusionResult:
+    """Per-frame fused lists (reference order) and NMS survivors (host arrays)."""
+
+    def __init__(self, boxes, conf, cls, src, origin, match, keep):
+        self.boxes, self.conf, self.cls, self.src, self.keep = boxes, conf, cls, src, keep
+        self.origin, self.match = origin, match
+
+
+def fuse_frames(frames, conf_threshold=0.3, fusion_iou_threshold=0.7, nms_threshold=0.5,
+                mode=_lib.FUSE_BAYES, apply_nms=True, device=None):
+    """frames: list of (yolo_boxes (n,4) int, yolo_conf (n,) f64, yolo_cls (n,) int,
+    sfa_boxes (m,4) int, sfa_conf (m,) f64).  Runs sfa_fuse_detections on the GPU."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    B = len(frames)
+    if B == 0:
+        return []
+    yb, yc, yk, sb, sc = [], [], [], [], []
+    yoff, soff = [0], [0]
+    for f in frames:
+        a, c, k, s, d = (np.asarray(v) for v in f)
+        yb.append(a.astype(np.int32).reshape(-1, 4))
+        yc.append(c.astype(np.float64).reshape(-1))
+        yk.append(k.astype(np.int32).reshape(-1))
+        sb.append(s.astype(np.int32).reshape(-1, 4))
+        sc.append(d.astype(np.float64).reshape(-1))
+        if yb[-1].shape[0] > 512 or sb[-1].shape[0] > 512:
+            raise ValueError("fusion: at most 512 boxes per side per frame")
+        yoff.append(yoff[-1] + yb[-1].shape[0])
+        soff.append(soff[-1] + sb[-1].shape[0])
+    t = lambda x, dt: torch.from_numpy(np.ascontiguousarray(np.concatenate(x) if x else x, dt)).to(dev)
+    Y, YC, YK = t(yb, np.int32), t(yc, np.float64), t(yk, np.int32)
+    S, SC = t(sb, np.int32), t(sc, np.float64)
+    YO = torch.tensor(yoff, dtype=torch.int32, device=dev)
+    SO = torch.tensor(soff, dtype=torch.int32, device=dev)
+    cap = max(1, yoff[-1] + soff[-1])
+    ob = torch.zeros((cap, 4), dtype=torch.int32, device=dev)
+    oc = torch.zeros(cap, dtype=torch.float64, device=dev)
+    ok = torch.zeros(cap, dtype=torch.int32, device=dev)
+    osrc = torch.zeros(cap, dtype=torch.int32, device=dev)
+    oorig = torch.zeros(cap, dtype=torch.int32, device=dev)
+    omatch = torch.zeros(cap, dtype=torch.int32, device=dev)
+    ocount = torch.zeros(B, dtype=torch.int32, device=dev)
+    okeep = torch.zeros(cap, dtype=torch.int32, device=dev)
+    okc = torch.zeros(B, dtype=torch.int32, device=dev)
+    prm = _lib.SfaFusionParams(float(conf_threshold), float(fusion_iou_threshold),
+                               float(nms_threshold), int(mode), 1 if apply_nms else 0)
+    ptr = lambda x: x.data_ptr() if x.numel() else None
+    check(lib().sfa_fuse_detections(B, ptr(Y), ptr(YC), ptr(YK), YO.data_ptr(), ptr(S), ptr(SC),
+                                    SO.data_ptr(), ctypes.byref(prm), ob.data_ptr(), oc.data_ptr(),
+                                    ok.data_ptr(), osrc.data_ptr(), oorig.data_ptr(),
+                                    omatch.data_ptr(), ocount.data_ptr(),
+                                    okeep.data_ptr(), okc.data_ptr(), _lib.stream_ptr(dev)),
+          "sfa_fuse_detections")
+    ob, oc, ok, osrc = ob.cpu().numpy(), oc.cpu().numpy(), ok.cpu().numpy(), osrc.cpu().numpy()
+    oorig, omatch = oorig.cpu().numpy(), omatch.cpu().numpy()
+    ocount, okeep, okc = ocount.cpu().numpy(), okeep.cpu().numpy(), okc.cpu().numpy()
+    out = []
+    for b in range(B):
+        base, n = yoff[b] + soff[b], int(ocount[b])
+        sl = slice(base, base + n)
+        keep = okeep[base: base + int(okc[b])].copy() if apply_nms else None
+        if n < 0:
+            raise ValueError(f"fusion: frame {b} exceeds 512 boxes per side")
+        out.append(FusionResult(ob[sl].copy(), oc[sl].copy(), ok[sl].copy(), osrc[sl].copy(),
+                                oorig[sl].copy(), omatch[sl].copy(), keep))
+    return out

@@ -35,6 +35,12 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def golden_fusion():
+    import numpy as np
+    return np.load(os.path.join(GOLDEN, "fusion_golden.npz"))
+
+
+@pytest.fixture(scope="session")
 def gpu():
     if not gpu_available():
         pytest.skip("no GPU visible")
