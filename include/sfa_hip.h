@@ -158,6 +158,66 @@ int sfa_decode(const float* hm, const float* off, const float* dir, const float*
                int apply_sigmoid, float* dets, void* workspace, size_t workspace_bytes,
                void* stream);
 
+/* ------------------------------------------------ post-processing on device --
+ * the SFA side of the fusion scripts without a host hop.
+ *
+ * sfa_post_process replaces utils/evaluation_utils.py:112-163 post_processing (for
+ * EVERY frame; the reference returns only the last one, :158) followed by :177-193
+ * convert_det_to_real_values.  dets: device f32 (B, K, 10) from sfa_decode.  Per frame
+ * the rows with class == j and score > peak_thresh (f32 compare), class-major, decode
+ * order within a class, are written compacted (frame b at out_offsets[b], a DEVICE
+ * int32 array of batch+1 entries written by the call):
+ *   out_preds f32 (n, 8) [score, x*down, y*down, z, h, w/bound_y*bev_w, l/bound_x*bev_h,
+ *                         atan2(dir0, dir1)]          (the post_processing dict rows)
+ *   out_real  f64 (n, 8) [class, x, y, z, h, w, l, yaw] (convert_det_to_real_values)
+ * convert_det_to_real_values works on numpy scalars, so its arithmetic type follows the
+ * numpy version: SFA_REAL_F32 = numpy >= 2 (f32, as the fixtures were generated),
+ * SFA_REAL_F64 = numpy 1.x (f64 from the f32 inputs; requirements.txt pins 1.18.3).
+ * Capacity: batch*K rows.  One workgroup (the work is a few hundred rows). */
+enum sfa_real_arith { SFA_REAL_F32 = 0, SFA_REAL_F64 = 1 };
+typedef struct sfa_post_params {
+  int num_classes;        /* 3 */
+  int down_ratio;         /* 4 */
+  float peak_thresh;      /* 0.2 */
+  int bev_h, bev_w;       /* 608, 608 (kitti_config.py BEV_HEIGHT / BEV_WIDTH) */
+  double bound_x, bound_y;            /* 50, 50 */
+  double min_x, min_y, min_z;         /* 0, -25, -2.73 */
+  int arith;              /* SFA_REAL_F32 | SFA_REAL_F64 */
+} sfa_post_params;
+int sfa_post_process(const float* dets, int batch, int K, const sfa_post_params* params,
+                     float* out_preds, double* out_real, int32_t* out_offsets, void* stream);
+
+/* sfa_project_boxes replaces test6.py:129-187 convert_sfa3d_to_2d_boxes (with
+ * data_process/transformation.py:99-107 lidar_to_camera_box): for each real row
+ * (CSR by DEVICE offsets) whose confidence >= conf_min — the confidence is column 0
+ * (the class id, as the reference reads it, test6.py:138) with SFA_CONF_CLASS_ID or the
+ * detection score (preds column 0) with SFA_CONF_SCORE — the 8 box corners are moved
+ * to the camera (V2C, R0), rotated by ry = -yaw - pi/2, projected with P2, clipped to
+ * the image like Python max(0, .) / min(img, .), and kept when max > min as int32
+ * [int(min_x), int(min_y), int(max_x - min_x), int(max_y - min_y)].
+ * Outputs compacted per frame (out_offsets, DEVICE int32 batch+1, written by the
+ * call): boxes int32 (m, 4), conf f64, out_row = the row index within the frame's
+ * real rows, out_extent (optional) f64 (m, 4) = clipped [min_x, min_y, max_x, max_y].
+ * calib: DEVICE array of `batch` sfa_calib (or one, when calib_per_frame = 0); the
+ * matrices are the calib file's values (f32 in the reference, widened to f64).
+ * f64 without contraction; numpy's BLAS and libm may differ in the last ulp. */
+enum sfa_conf_source { SFA_CONF_CLASS_ID = 0, SFA_CONF_SCORE = 1 };
+typedef struct sfa_calib {
+  double V2C[12];  /* Tr_velo_to_cam 3x4, row-major */
+  double R0[9];    /* R_rect 3x3 */
+  double P2[12];   /* 3x4 */
+  int32_t img_h, img_w;
+} sfa_calib;
+typedef struct sfa_project_params {
+  double conf_min;      /* 0.3 */
+  int conf_source;      /* SFA_CONF_CLASS_ID | SFA_CONF_SCORE */
+  int calib_per_frame;  /* 1: calib[b] per frame; 0: calib[0] for all */
+} sfa_project_params;
+int sfa_project_boxes(const double* real, const float* preds, const int32_t* offsets, int batch,
+                      const sfa_calib* calib, const sfa_project_params* params,
+                      int32_t* out_boxes, double* out_conf, int32_t* out_row, double* out_extent,
+                      int32_t* out_offsets, void* stream);
+
 /* ------------------------------------------------------------ fusion --
  * Camera-LiDAR late fusion + NMS.  Replaces test6.py:310-348
  * create_fused_detections_wrapper -> :231-308 bayesian_inspired_fuse_overlapping_detections

@@ -84,6 +84,33 @@ _PROTOS["sfa_iou_matrix"] = (_c_int, [_vp, _c_int, _vp, _c_int, _vp, _vp])
 _PROTOS["sfa_fuse_detections"] = (_c_int, [_c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                            ctypes.POINTER(SfaFusionParams), _vp, _vp, _vp, _vp,
                                            _vp, _vp, _vp, _vp, _vp, _vp])
+
+
+class SfaPostParams(ctypes.Structure):
+    _fields_ = [("num_classes", ctypes.c_int), ("down_ratio", ctypes.c_int),
+                ("peak_thresh", ctypes.c_float), ("bev_h", ctypes.c_int), ("bev_w", ctypes.c_int),
+                ("bound_x", ctypes.c_double), ("bound_y", ctypes.c_double),
+                ("min_x", ctypes.c_double), ("min_y", ctypes.c_double), ("min_z", ctypes.c_double),
+                ("arith", ctypes.c_int)]
+
+
+class SfaCalib(ctypes.Structure):
+    _fields_ = [("V2C", ctypes.c_double * 12), ("R0", ctypes.c_double * 9),
+                ("P2", ctypes.c_double * 12), ("img_h", ctypes.c_int32), ("img_w", ctypes.c_int32)]
+
+
+class SfaProjectParams(ctypes.Structure):
+    _fields_ = [("conf_min", ctypes.c_double), ("conf_source", ctypes.c_int),
+                ("calib_per_frame", ctypes.c_int)]
+
+
+REAL_F32, REAL_F64 = 0, 1
+CONF_CLASS_ID, CONF_SCORE = 0, 1
+_PROTOS["sfa_post_process"] = (_c_int, [_vp, _c_int, _c_int, ctypes.POINTER(SfaPostParams), _vp,
+                                        _vp, _vp, _vp])
+_PROTOS["sfa_project_boxes"] = (_c_int, [_vp, _vp, _vp, _c_int, _vp,
+                                         ctypes.POINTER(SfaProjectParams), _vp, _vp, _vp, _vp,
+                                         _vp, _vp])
 EXPORTED_SYMBOLS = tuple(_PROTOS)
 
 _lib = None

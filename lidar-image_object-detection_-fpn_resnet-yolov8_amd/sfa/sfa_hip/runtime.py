@@ -432,3 +432,94 @@ def fuse_frames(frames, conf_threshold=0.3, fusion_iou_threshold=0.7, nms_thresh
         out.append(FusionResult(ob[sl].copy(), oc[sl].copy(), ok[sl].copy(), osrc[sl].copy(),
                                 oorig[sl].copy(), omatch[sl].copy(), keep))
     return out
+
+
+# ------------------------------------------------- post-processing on device
+def make_calib(V2C, R0, P2, img_shape) -> "_lib.SfaCalib":
+    """One frame's calibration (kitti_data_utils.py:127-139 Calibration fields: V2C 3x4,
+    R0 3x3, P2 3x4 — f32 in the reference, widened exactly) + image shape (rows, cols)."""
+    c = _lib.SfaCalib()
+    c.V2C[:] = [float(v) for v in np.asarray(V2C, np.float64).reshape(-1)[:12]]
+    c.R0[:] = [float(v) for v in np.asarray(R0, np.float64)[:3, :3].reshape(-1)]
+    c.P2[:] = [float(v) for v in np.asarray(P2, np.float64).reshape(-1)[:12]]
+    c.img_h, c.img_w = int(img_shape[0]), int(img_shape[1])
+    return c
+
+
+def calib_tensor(calibs, device) -> torch.Tensor:
+    """list of SfaCalib -> device bytes (the C struct array)."""
+    arr = (_lib.SfaCalib * len(calibs))(*calibs)
+    host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+    return host.to(device)
+
+
+def post_params(num_classes=3, down_ratio=4, peak_thresh=0.2, arith=_lib.REAL_F32,
+                boundary=DEFAULT_BOUNDARY, bev_hw=(608, 608)) -> "_lib.SfaPostParams":
+    p = _lib.SfaPostParams()
+    p.num_classes, p.down_ratio, p.peak_thresh = int(num_classes), int(down_ratio), float(peak_thresh)
+    p.bev_h, p.bev_w = int(bev_hw[0]), int(bev_hw[1])
+    p.bound_x = float(boundary["maxX"] - boundary["minX"])
+    p.bound_y = float(boundary["maxY"] - boundary["minY"])
+    p.min_x, p.min_y, p.min_z = (float(boundary[k]) for k in ("minX", "minY", "minZ"))
+    p.arith = int(arith)
+    return p
+
+
+def post_process(dets: torch.Tensor, num_classes=3, down_ratio=4, peak_thresh=0.2,
+                 arith=_lib.REAL_F32, boundary=DEFAULT_BOUNDARY, bev_hw=(608, 608), out=None):
+    """post_processing (evaluation_utils.py:112-163, every frame) + convert_det_to_real_values
+    (:177-193) on the GPU.  dets (B, K, 10) f32 -> (preds (B*K, 8) f32, real (B*K, 8) f64,
+    offsets (B+1,) int32), all device tensors; frame b owns rows offsets[b]:offsets[b+1]."""
+    dets = _require_gpu_tensor(dets, "post_process")
+    B, K = int(dets.shape[0]), int(dets.shape[1])
+    if dets.dim() != 3 or dets.shape[2] != 10:
+        raise ValueError("post_process: dets must be (B, K, 10)")
+    dev = dets.device
+    if out is None:
+        out = (torch.empty((max(1, B * K), 8), dtype=torch.float32, device=dev),
+               torch.empty((max(1, B * K), 8), dtype=torch.float64, device=dev),
+               torch.empty(B + 1, dtype=torch.int32, device=dev))
+    preds, real, off = out
+    prm = post_params(num_classes, down_ratio, peak_thresh, arith, boundary, bev_hw)
+    check(lib().sfa_post_process(dets.data_ptr(), B, K, ctypes.byref(prm), preds.data_ptr(),
+                                 real.data_ptr(), off.data_ptr(), _lib.stream_ptr(dev)),
+          "sfa_post_process")
+    return preds, real, off
+
+
+def project_boxes(real: torch.Tensor, offsets: torch.Tensor, calibs, preds=None, conf_min=0.3,
+                  conf_source=_lib.CONF_CLASS_ID, extents=False, out=None):
+    """convert_sfa3d_to_2d_boxes (test6.py:129-187) on the GPU for every frame.
+    calibs: a device tensor from calib_tensor() or a list of SfaCalib (one per frame, or
+    one for all).  Returns (boxes (cap, 4) int32, conf f64, row int32, extent f64 or None,
+    offsets (B+1,) int32) device tensors (cap = number of real rows)."""
+    real = _require_gpu_tensor(real, "project_boxes", torch.float64)
+    offsets = _require_gpu_tensor(offsets, "project_boxes offsets", torch.int32)
+    dev = real.device
+    B = int(offsets.numel()) - 1
+    if isinstance(calibs, torch.Tensor):
+        ct = calibs
+        n_cal = ct.numel() // ctypes.sizeof(_lib.SfaCalib)
+    else:
+        calibs = list(calibs)
+        ct, n_cal = calib_tensor(calibs, dev), len(calibs)
+    if n_cal not in (1, B) or n_cal == 0:
+        raise ValueError("project_boxes: need one calibration or one per frame")
+    if conf_source == _lib.CONF_SCORE:
+        preds = _require_gpu_tensor(preds, "project_boxes preds")
+    cap = max(1, real.shape[0])
+    if out is None:
+        out = (torch.empty((cap, 4), dtype=torch.int32, device=dev),
+               torch.empty(cap, dtype=torch.float64, device=dev),
+               torch.empty(cap, dtype=torch.int32, device=dev),
+               torch.empty((cap, 4), dtype=torch.float64, device=dev) if extents else None,
+               torch.empty(B + 1, dtype=torch.int32, device=dev))
+    boxes, conf, row, ext, off = out
+    prm = _lib.SfaProjectParams(float(conf_min), int(conf_source), 1 if n_cal == B and B > 1 else 0)
+    check(lib().sfa_project_boxes(real.data_ptr(), preds.data_ptr() if preds is not None else None,
+                                  offsets.data_ptr(), B, ct.data_ptr(), ctypes.byref(prm),
+                                  boxes.data_ptr(), conf.data_ptr(), row.data_ptr(),
+                                  ext.data_ptr() if ext is not None else None, off.data_ptr(),
+                                  _lib.stream_ptr(dev)),
+          "sfa_project_boxes")
+    return boxes, conf, row, ext, off

@@ -41,6 +41,12 @@ def golden_fusion():
 
 
 @pytest.fixture(scope="session")
+def golden_project():
+    import numpy as np
+    return np.load(os.path.join(GOLDEN, "project_golden.npz"))
+
+
+@pytest.fixture(scope="session")
 def gpu():
     if not gpu_available():
         pytest.skip("no GPU visible")
