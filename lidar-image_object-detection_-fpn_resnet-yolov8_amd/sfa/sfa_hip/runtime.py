@@ -497,6 +497,8 @@ def project_boxes(real: torch.Tensor, offsets: torch.Tensor, calibs, preds=None,
     offsets = _require_gpu_tensor(offsets, "project_boxes offsets", torch.int32)
     dev = real.device
     B = int(offsets.numel()) - 1
+    if real.shape[0] == 0:  # no rows: the offsets are all 0, nothing is read
+        real = torch.zeros((1, 8), dtype=torch.float64, device=dev)
     if isinstance(calibs, torch.Tensor):
         ct = calibs
         n_cal = ct.numel() // ctypes.sizeof(_lib.SfaCalib)

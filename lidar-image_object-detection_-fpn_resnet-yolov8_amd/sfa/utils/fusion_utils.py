@@ -11,6 +11,7 @@ to the Python loops; ``fuse_frames`` batches many frames in one launch.
 from __future__ import annotations
 
 import numpy as np
+import torch
 
 from sfa_hip import _lib, runtime
 
@@ -120,3 +121,23 @@ def fuse_frames(frames, confidence_threshold=0.3, fusion_iou_threshold=0.7, nms_
     """Batched form: many frames in one launch -> list of runtime.FusionResult."""
     return runtime.fuse_frames(frames, confidence_threshold, fusion_iou_threshold, nms_threshold,
                                _lib.FUSE_WEIGHTED if weighted else _lib.FUSE_BAYES, apply_nms=True)
+
+
+def convert_sfa3d_to_2d_boxes(sfa_detections, calib, img_shape, device=None):
+    """test6.py:129-187: post_processing's per-class dict -> (list of int [x, y, w, h] image
+    boxes, list of confidences).  As in the reference the "confidence" is column 0 of
+    convert_det_to_real_values, i.e. the class id, so class 0 rows never pass the 0.3 cut.
+    The metres conversion is the host API (evaluation_utils.py:177-193); the camera
+    transform, corner projection and clipping run on the GPU (sfa_project_boxes).
+    ``calib`` needs the Calibration attributes V2C (3x4), R0 (3x3), P2 (3x4)."""
+    from utils.evaluation_utils import convert_det_to_real_values
+    real = np.asarray(convert_det_to_real_values(sfa_detections), np.float64).reshape(-1, 8)
+    if len(real) == 0:
+        return [], []
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    off = torch.tensor([0, len(real)], dtype=torch.int32, device=dev)
+    cal = runtime.make_calib(calib.V2C, calib.R0, calib.P2, img_shape)
+    boxes, conf, _, _, boff = runtime.project_boxes(torch.from_numpy(real).to(dev), off, [cal])
+    n = int(boff[1].item())
+    return ([[int(v) for v in b] for b in boxes[:n].cpu().numpy()],
+            [float(c) for c in conf[:n].cpu().numpy()])

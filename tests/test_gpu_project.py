@@ -150,3 +150,20 @@ def test_empty_and_errors(gpu):
     assert off.cpu().tolist() == [0, 0, 0]
     with pytest.raises(_lib.SfaNativeError):
         runtime.post_process(torch.zeros((1, 5, 10)))  # CPU tensor: no fallback
+
+
+def test_dropin_convert_sfa3d_to_2d_boxes(golden_project, gpu):
+    from utils.fusion_utils import convert_sfa3d_to_2d_boxes
+
+    class Calib:
+        pass
+    g = golden_project
+    for name in ("typical", "edges"):
+        for b, cal_name in enumerate(g[f"{name}/calibs"]):
+            c = Calib()
+            c.V2C, c.R0, c.P2 = (g[f"calib/{cal_name}/{f}"] for f in ("V2C", "R0", "P2"))
+            shape = tuple(int(v) for v in g[f"calib/{cal_name}/img_shape"])
+            post = {j: g[f"{name}/{b}/post{j}"] for j in range(3)}
+            boxes, conf = convert_sfa3d_to_2d_boxes(post, c, shape)
+            np.testing.assert_array_equal(np.array(boxes, np.int64).reshape(-1, 4), g[f"{name}/{b}/boxes"])
+            np.testing.assert_array_equal(np.array(conf), g[f"{name}/{b}/conf"])
