@@ -2,8 +2,9 @@
 """Benchmark of the MI355X hot path — BEV frames/s at 608x608, bs=16 per GPU.
 
 One step = one batch of 16 synthetic 3x608x608 BEV frames, resident in HBM,
-through the KFPN FPN-ResNet-18 forward (23 fp32-MFMA implicit-GEMM conv launches
-+ maxpool / upsample / KFPN kernels) and the fused sigmoid + decode (K=50), each
+through the KFPN FPN-ResNet-18 forward (23 implicit-GEMM conv launches — bf16x6
+split-operand MFMA by default, ``--math f32`` for the f32 MFMA kernels — + maxpool /
+upsample / KFPN kernels) and the fused sigmoid + decode (K=50), each
 captured as a HIP graph; with N > 1 the step also all-gathers the (16, 50, 10)
 detections over RCCL (frames are sharded: rank r owns its own 16 frames).
 ``--workload e2e`` starts each step from raw point clouds (BEV voxelisation on
@@ -38,6 +39,9 @@ from sfa_hip.runtime import (DEFAULT_HEADS, DetectorPipeline, KfpnEngine,  # noq
 CONV_MACS_PER_FRAME = 31_283_555_328
 CONV_FLOP_PER_FRAME = 2 * CONV_MACS_PER_FRAME
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, dense
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
+# bf16x6 computes each f32 MAC as 6 bf16 MFMA products: its f32-equivalent ceiling
+PEAK_BF16X6_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
 METRIC = "BEV frames/sec (608x608, bs=16)"
 
 
@@ -49,6 +53,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--K", type=int, default=50)
     ap.add_argument("--workload", choices=["bev_infer", "e2e"], default="bev_infer")
+    ap.add_argument("--math", choices=["bf16x6", "f32"],
+                    default="f32" if _lib.math_from_env() == _lib.MATH_F32 else "bf16x6",
+                    help="convolution arithmetic (include/sfa_hip.h sfa_math; default bf16x6)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=4, help="frames timed for the CPU baseline")
@@ -79,7 +86,8 @@ def build_pipeline(dev, args, rank):
     arch = _lib.make_arch(DEFAULT_HEADS)
     spec = _lib.state_layout(arch)
     sd = synthetic.synthetic_state_dict(spec, seed=0)
-    engine = KfpnEngine(arch, pack_state_dict(sd, arch), dev)
+    engine = KfpnEngine(arch, pack_state_dict(sd, arch), dev,
+                        math=_lib.MATH_F32 if args.math == "f32" else _lib.MATH_BF16X6)
     if args.workload == "e2e":
         clouds = [synthetic.synthetic_point_cloud(1000 * rank + i + 1) for i in range(args.batch)]
         pipe = DetectorPipeline(engine, args.batch, K=args.K, with_bev=True,
@@ -143,7 +151,9 @@ def traffic_per_forward(args):
     if args.workload != "bev_infer" or args.batch != 16:
         return None
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_forward.json")))
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_forward_{args.math}.json")))
+    if not files and args.math == "f32":
+        files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_forward.json")))
     if not files:
         return None
     with open(files[-1]) as f:
@@ -229,6 +239,8 @@ def main():
     if rank == 0:
         flop_step = CONV_FLOP_PER_FRAME * args.batch
         achieved = flop_step / (fwd_ms * 1e-3) / 1e12
+        x6 = args.math == "bf16x6"
+        peak = PEAK_BF16X6_TFLOPS if x6 else PEAK_FP32_MFMA_TFLOPS
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -240,7 +252,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "f32 (bf16x6: operands split into 3 bf16 terms, 6 products, f32 accumulate)"
+                     if x6 else "f32",
             "data": "synthetic (hash-RNG U[0,1) BEV frames; synthetic He-uniform weights, BN folded)"
                     if args.workload == "bev_infer" else
                     "synthetic (132,880-pt LiDAR sweeps per frame, SURVEY §8(d); synthetic weights)",
@@ -258,12 +271,16 @@ def main():
             "stages_ms": {"forward": round(fwd_ms, 4), "decode": round(dec_ms, 4)},
             "roofline": {
                 "bound": "mfma",
-                "kernel": "conv_mfma_kernel (23 implicit-GEMM launches per forward; achieved uses "
-                          "the whole forward's event time, aux kernels included)",
+                "kernel": ("conv_x6_kernel / conv_x6g_kernel" if x6 else "conv_mfma_kernel") +
+                          " (23 implicit-GEMM launches per forward; achieved = algorithmic f32 FLOP "
+                          "over the whole forward's event time, aux kernels included)",
                 "achieved": round(achieved, 3),
-                "peak": PEAK_FP32_MFMA_TFLOPS,
+                "peak": round(peak, 2),
+                "peak_basis": ("dense bf16 MFMA 2500 TF / 6 bf16 products per f32 MAC" if x6 else
+                               "dense f32 MFMA (v_mfma_f32_32x32x2_f32)"),
                 "unit": "TFLOP/s",
-                "frac": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                "frac": round(achieved / peak, 4),
+                "frac_of_f32_mfma_peak": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
                 "traffic": traffic_per_forward(args),
                 "algorithmic_flop_per_step": flop_step,
             },

@@ -102,7 +102,8 @@ int sfa_state_entry(const sfa_arch* arch, int index, char* name, int name_len, i
  * state_dict entry except *.num_batches_tracked, concatenated in
  * sfa_state_entry order.  BatchNorm (eps 1e-5) is folded into the preceding
  * convolution; conv weights are re-laid out OHWI / K-concatenated for the
- * implicit-GEMM kernels.  `packed` must hold sfa_packed_floats(arch) floats. */
+ * implicit-GEMM kernels, each also stored as three bf16 terms for SFA_MATH_BF16X6.
+ * `packed` must hold sfa_packed_floats(arch) floats. */
 size_t sfa_state_floats(const sfa_arch* arch);
 size_t sfa_packed_floats(const sfa_arch* arch);
 int sfa_pack_weights(const sfa_arch* arch, const float* state, size_t state_floats, float* packed);
@@ -112,6 +113,16 @@ int sfa_pack_weights(const sfa_arch* arch, const float* state, size_t state_floa
 typedef struct sfa_model sfa_model;
 int sfa_model_create(const sfa_arch* arch, const float* packed_device, sfa_model** out);
 void sfa_model_destroy(sfa_model* model);
+
+/* Arithmetic of the convolutions (all results are f32; both modes meet the parity
+ * bar):
+ *   SFA_MATH_BF16X6 (default) — every f32 operand split into three bf16 terms, the six
+ *     significant products on bf16 MFMA with f32 accumulation: f32-level accuracy at
+ *     ~2.7x the f32-MFMA rate (max rel. logit error vs the reference ~3e-6);
+ *   SFA_MATH_F32 — v_mfma_f32_32x32x2_f32 (exact f32 FMA chains). */
+enum sfa_math { SFA_MATH_F32 = 0, SFA_MATH_BF16X6 = 1 };
+int sfa_model_set_math(sfa_model* model, int math);
+int sfa_model_get_math(const sfa_model* model);
 
 /* Forward.  x: device float32, layout SFA_IN_NCHW3 (B,3,H,W) as the reference
  * takes it, or SFA_IN_NHWC4 (B,H,W,4) as sfa_bev_voxelize writes it.

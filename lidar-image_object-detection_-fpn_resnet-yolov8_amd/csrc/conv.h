@@ -53,6 +53,7 @@ struct ConvArgs {
   int kseg1;           // first K index of segment 1 (multiple of 16)
   int Kpad;            // total K (multiple of 16)
   const float* w;      // [N][Kpad] (OHWI per segment, K-concatenated, zero padded)
+  const uint16_t* wx;  // bf16x6 path: w split into 3 bf16 terms, [3][N][Kpad]
   const float* bias;   // [N]
   const float* res;    // residual [M][N] (NHWC) or nullptr
   float* y;            // output [M][N] (NHWC)
@@ -68,6 +69,6 @@ struct ConvArgs {
   float* hout;
 };
 
-int launch_conv(const ConvArgs& a, int epilogue, hipStream_t stream);
+int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t stream);
 
 }  // namespace sfa

@@ -1,10 +1,34 @@
-// Convolution dispatch: picks the conv_mfma_kernel tile configuration per layer
-// shape (see conv_kernel.h for the kernel; DESIGN.md §5 for the rooflines).
+// Convolution dispatch: picks the kernel (f32 MFMA or bf16x6) and its tile
+// configuration per layer shape (conv_kernel.h, conv_x6_kernel.h).
 #include "conv_kernel.h"
+#include "conv_x6_kernel.h"
 
 namespace sfa {
 
-int launch_conv(const ConvArgs& a, int epilogue, hipStream_t st) {
+// bf16x6 tiles per shape, from tools/convbench.hip sweeps on MI355X (round 1):
+// wide-N tiles amortise the A split; 8-wave LDS-DMA tiles for the big-M layers.
+// Returns SFA_E_UNSUPPORTED when no bf16x6 tile fits (the caller falls back to f32).
+static int launch_conv_x6(const ConvArgs& a, int epilogue, hipStream_t st) {
+  if (!a.wx) return SFA_E_UNSUPPORTED;
+  auto ok = [](int rc) { return rc != SFA_E_UNSUPPORTED; };
+  int rc = SFA_E_UNSUPPORTED;
+  if (epilogue == EPI_HEAD) {
+    if (a.N == 320) rc = launch_conv_x6g_cfg<256, 320, 32, EPI_HEAD, 1>(a, st);
+    if (!ok(rc)) rc = launch_conv_x6_cfg<128, 64, 32, 64, 32, EPI_HEAD, 2>(a, st);
+    if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_HEAD, 1>(a, st);
+    return rc;
+  }
+  if (a.N == 64) return launch_conv_x6g_cfg<256, 64, 32, EPI_STD, 1>(a, st);
+  if (a.N % 128 == 0) {
+    if (a.M >= 50000) rc = launch_conv_x6_cfg<128, 128, 64, 64, 16, EPI_STD, 2>(a, st);
+    else if (a.M >= 10000) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2>(a, st);
+    else rc = launch_conv_x6_cfg<64, 128, 32, 64, 32, EPI_STD, 2>(a, st);
+    if (!ok(rc)) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2>(a, st);
+  }
+  return rc;
+}
+
+int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t st) {
   // Host-side shape checks: the kernels assume these and never bounds-check them.
   if (a.N <= 0 || a.N % 64 != 0 || a.M <= 0 || a.Kpad <= 0 || a.Kpad % 16 != 0) {
     set_error("conv: unsupported shape M=%d N=%d Kpad=%d", a.M, a.N, a.Kpad);
@@ -28,6 +52,10 @@ int launch_conv(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (a.nseg == 2 && (a.kseg1 % 16 != 0 || a.kseg1 <= 0 || a.kseg1 >= a.Kpad)) {
     set_error("conv: bad kseg1 %d", a.kseg1);
     return SFA_E_UNSUPPORTED;
+  }
+  if (math == SFA_MATH_BF16X6) {
+    const int rc = launch_conv_x6(a, epilogue, st);
+    if (rc != SFA_E_UNSUPPORTED) return rc;
   }
   // Tile choice per shape, from tools/convbench.hip sweeps on MI355X (round 1):
   // 32x64 / 32x32 wave tiles at 4 waves per SIMD hide the gather latency best;

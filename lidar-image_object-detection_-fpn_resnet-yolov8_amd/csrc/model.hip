@@ -117,12 +117,14 @@ static std::vector<Entry> state_layout(const sfa_arch* a) {
 }
 
 // ----------------------------------------------------------- packed layout
+// Offsets in floats into the packed buffer.  wx: the same weights split into three
+// bf16 terms [3][N][Kpad] for the bf16x6 kernels (conv_x6_kernel.h).
 struct PConv {
-  size_t w, b;
+  size_t w, b, wx;
   int N, K, Kpad;
 };
 struct PHeads {
-  size_t w3, b3, w1, b1;
+  size_t w3, b3, w1, b1, wx;
   int N, K;
 };
 struct Plan {
@@ -148,6 +150,7 @@ static Plan make_plan(const sfa_arch* a) {
     c.Kpad = (int)align_up(K, 16);
     c.w = take((size_t)N * c.Kpad);
     c.b = take(N);
+    c.wx = take(((size_t)3 * N * c.Kpad + 1) / 2);
     return c;
   };
   p.stem = conv(64, 49 * 4);
@@ -173,6 +176,7 @@ static Plan make_plan(const sfa_arch* a) {
     h.b3 = take(h.N);
     h.w1 = take((size_t)a->num_heads * 4 * 64);
     h.b1 = take((size_t)a->num_heads * 4);
+    h.wx = take(((size_t)3 * h.N * h.K + 1) / 2);
   }
   p.total = cur;
   return p;
@@ -212,6 +216,29 @@ static void bn_fold(const StateView& s, const std::string& p, int C, std::vector
   }
 }
 
+// f32 -> bf16, round to nearest even (finite inputs)
+static uint16_t bf16_rne(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// W (n floats) -> three bf16 terms t0 + t1 + t2 == W (each residual is exact in f32)
+static void split_terms(const float* w, size_t n, uint16_t* out) {
+  for (size_t i = 0; i < n; ++i) {
+    float x = w[i];
+    for (int t = 0; t < 3; ++t) {
+      const uint16_t b = bf16_rne(x);
+      out[t * n + i] = b;
+      uint32_t u = (uint32_t)b << 16;
+      float bf;
+      memcpy(&bf, &u, 4);
+      x -= bf;
+    }
+  }
+}
+
 }  // namespace sfa
 
 using namespace sfa;
@@ -220,6 +247,7 @@ struct sfa_model {
   sfa_arch arch;
   const float* w;
   Plan plan;
+  int math;
 };
 
 extern "C" int sfa_abi_version(void) { return SFA_ABI_VERSION; }
@@ -331,6 +359,18 @@ extern "C" int sfa_pack_weights(const sfa_arch* arch, const float* state, size_t
       }
     }
   }
+  // bf16x6 terms of every implicit-GEMM weight matrix
+  auto split = [&](const PConv& c) {
+    split_terms(packed + c.w, (size_t)c.N * c.Kpad, reinterpret_cast<uint16_t*>(packed + c.wx));
+  };
+  split(p.stem);
+  for (int li = 0; li < 4; ++li)
+    for (int bi = 0; bi < 2; ++bi)
+      for (int ci = 0; ci < 2; ++ci) split(p.blk[li][bi][ci]);
+  for (int i = 0; i < 3; ++i) split(p.fpn[i]);
+  for (int f = 0; f < 3; ++f)
+    split_terms(packed + p.heads[f].w3, (size_t)p.heads[f].N * p.heads[f].K,
+                reinterpret_cast<uint16_t*>(packed + p.heads[f].wx));
   return SFA_OK;
 }
 
@@ -342,11 +382,21 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   m->arch = *arch;
   m->w = packed_device;
   m->plan = make_plan(arch);
+  m->math = SFA_MATH_BF16X6;
   *out = m;
   return SFA_OK;
 }
 
 extern "C" void sfa_model_destroy(sfa_model* model) { delete model; }
+
+extern "C" int sfa_model_set_math(sfa_model* model, int math) {
+  SFA_CHECK_ARG(model, "set_math: null model");
+  SFA_CHECK_ARG(math == SFA_MATH_F32 || math == SFA_MATH_BF16X6, "set_math: unknown mode %d", math);
+  model->math = math;
+  return SFA_OK;
+}
+
+extern "C" int sfa_model_get_math(const sfa_model* model) { return model ? model->math : -1; }
 
 namespace sfa {
 
@@ -403,6 +453,7 @@ static ConvArgs conv_args(const float* wbase, const PConv& pc, int B, int OH, in
   a.nseg = 1;
   a.Kpad = pc.Kpad;
   a.w = wbase + pc.w;
+  a.wx = reinterpret_cast<const uint16_t*>(wbase + pc.wx);
   a.bias = wbase + pc.b;
   a.res = res;
   a.y = y;
@@ -476,7 +527,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   {
     ConvArgs a = conv_args(wb, p.stem, B, H2, W2, F(bf.s0), nullptr, 1);
     a.seg[0] = seg(xin, B, H, W, 4, 7, 2, 3);
-    SFA_RC(launch_conv(a, EPI_STD, st));
+    SFA_RC(launch_conv(a, EPI_STD, m->math, st));
   }
   SFA_RC(launch_maxpool3s2(F(bf.s0), F(bf.p0), B, H2, W2, 64, st));  // :182
   // residual layers (fpn_resnet.py:184-187)
@@ -493,7 +544,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     {
       ConvArgs a = conv_args(wb, p.blk[li][0][0], B, oh, ow, t, nullptr, 1);
       a.seg[0] = seg(xcur, B, h, w, cin, 3, stride, 1);
-      SFA_RC(launch_conv(a, EPI_STD, st));
+      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     {
       ConvArgs a = conv_args(wb, p.blk[li][0][1], B, oh, ow, av, li == 0 ? xcur : nullptr, 1);
@@ -503,18 +554,18 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
         a.kseg1 = 9 * planes;
         a.seg[1] = seg(xcur, B, h, w, cin, 1, stride, 0);
       }
-      SFA_RC(launch_conv(a, EPI_STD, st));
+      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     // block 1
     {
       ConvArgs a = conv_args(wb, p.blk[li][1][0], B, oh, ow, t, nullptr, 1);
       a.seg[0] = seg(av, B, oh, ow, planes, 3, 1, 1);
-      SFA_RC(launch_conv(a, EPI_STD, st));
+      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     {
       ConvArgs a = conv_args(wb, p.blk[li][1][1], B, oh, ow, lv, av, 1);
       a.seg[0] = seg(t, B, oh, ow, planes, 3, 1, 1);
-      SFA_RC(launch_conv(a, EPI_STD, st));
+      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     xcur = lv;
     h = oh;
@@ -531,7 +582,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.kseg1 = 512;
     a.seg[0] = seg(F(bf.up1), B, H16, W16, 512, 1, 1, 0);
     a.seg[1] = seg(F(bf.l[2]), B, H16, W16, 256, 1, 1, 0);
-    SFA_RC(launch_conv(a, EPI_STD, st));
+    SFA_RC(launch_conv(a, EPI_STD, m->math, st));
   }
   SFA_RC(launch_upsample2x(F(bf.c1), F(bf.up2), B, H16, W16, 256, st));
   {
@@ -540,7 +591,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.kseg1 = 256;
     a.seg[0] = seg(F(bf.up2), B, H8, W8, 256, 1, 1, 0);
     a.seg[1] = seg(F(bf.l[1]), B, H8, W8, 128, 1, 1, 0);
-    SFA_RC(launch_conv(a, EPI_STD, st));
+    SFA_RC(launch_conv(a, EPI_STD, m->math, st));
   }
   SFA_RC(launch_upsample2x(F(bf.c2), F(bf.up3), B, H8, W8, 128, st));
   {
@@ -549,7 +600,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.kseg1 = 128;
     a.seg[0] = seg(F(bf.up3), B, H4, W4, 128, 1, 1, 0);
     a.seg[1] = seg(F(bf.l[0]), B, H4, W4, 64, 1, 1, 0);
-    SFA_RC(launch_conv(a, EPI_STD, st));
+    SFA_RC(launch_conv(a, EPI_STD, m->math, st));
   }
   // Detection heads (fpn_resnet.py:219-233): per level all heads in one launch,
   // conv3x3 -> ReLU -> conv1x1 fused; channel-planar level outputs.
@@ -570,6 +621,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.seg[0] = seg(lin[f], B, lh[f], lw[f], kFpnC[f], 3, 1, 1);
     a.Kpad = hp.K;
     a.w = wb + hp.w3;
+    a.wx = reinterpret_cast<const uint16_t*>(wb + hp.wx);
     a.bias = wb + hp.b3;
     a.M = B * lh[f] * lw[f];
     a.N = hp.N;
@@ -583,7 +635,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       a.hoff[j] = hoff[j];
     }
     a.hout = lout[f];
-    SFA_RC(launch_conv(a, EPI_HEAD, st));
+    SFA_RC(launch_conv(a, EPI_HEAD, m->math, st));
   }
   // apply_kfpn (fpn_resnet.py:248-254)
   KfpnOut ko;

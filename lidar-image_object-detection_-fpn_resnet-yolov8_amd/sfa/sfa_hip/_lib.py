@@ -72,6 +72,23 @@ _PROTOS = {
                             _vp, _vp, _c_size, _vp]),
 }
 
+MATH_F32, MATH_BF16X6 = 0, 1
+_PROTOS["sfa_model_set_math"] = (_c_int, [_vp, _c_int])
+_PROTOS["sfa_model_get_math"] = (_c_int, [_vp])
+
+
+def math_from_env(default=MATH_BF16X6) -> int:
+    """SFA_MATH=f32 | bf16x6 selects the convolution arithmetic (include/sfa_hip.h)."""
+    v = os.environ.get("SFA_MATH", "").strip().lower()
+    if not v:
+        return default
+    if v in ("f32", "fp32"):
+        return MATH_F32
+    if v in ("bf16x6", "x6"):
+        return MATH_BF16X6
+    raise ValueError(f"SFA_MATH={v!r}: expected 'f32' or 'bf16x6'")
+
+
 class SfaFusionParams(ctypes.Structure):
     _fields_ = [("conf_threshold", ctypes.c_double), ("fusion_iou_threshold", ctypes.c_double),
                 ("nms_threshold", ctypes.c_double), ("mode", ctypes.c_int),

@@ -62,7 +62,7 @@ def pack_state_dict(state: dict, arch) -> np.ndarray:
 class KfpnEngine:
     """A device copy of the packed weights + an sfa_model handle + workspace cache."""
 
-    def __init__(self, arch, packed_host: np.ndarray, device):
+    def __init__(self, arch, packed_host: np.ndarray, device, math=None):
         self.arch = arch
         self.device = torch.device(device)
         self.heads = [(arch.head_names[j].value.decode(), int(arch.head_channels[j]))
@@ -73,6 +73,12 @@ class KfpnEngine:
               "sfa_model_create")
         self._h = h
         self._ws = {}
+        self.set_math(_lib.math_from_env() if math is None else math)
+
+    def set_math(self, math: int):
+        """_lib.MATH_BF16X6 (default) or _lib.MATH_F32 for every convolution."""
+        check(lib().sfa_model_set_math(self._h, int(math)), "sfa_model_set_math")
+        self.math = int(math)
 
     def __del__(self):
         try:

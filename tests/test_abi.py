@@ -61,6 +61,7 @@ def _unpack_plan_offsets(arch):
     def conv(key, N, K):
         Kp = (K + 15) // 16 * 16
         out[key] = (take(N * Kp), take(N), N, Kp)
+        out[key + "/wx"] = take((3 * N * Kp + 1) // 2)  # bf16x6 terms [3][N][Kpad]
 
     conv("stem", 64, 196)
     inpl = 64
@@ -111,6 +112,17 @@ def test_pack_weights_folds_batchnorm(golden):
     w_off, b_off, N, Kp = offs["fpn0"]
     np.testing.assert_array_equal(packed[w_off:w_off + N * Kp].reshape(N, Kp),
                                   sd["conv_up_level1.weight"][:, :, 0, 0])
+    # bf16x6 terms: three bf16 values (round to nearest even) summing exactly to W
+    for key in ("stem", "l1b0c2", "l3b1c2", "fpn0"):
+        w_off, _, N, Kp = offs[key]
+        W = packed[w_off:w_off + N * Kp]
+        x = offs[key + "/wx"]
+        t = packed[x:x + (3 * N * Kp + 1) // 2].view(np.uint16)[:3 * N * Kp].reshape(3, -1)
+        f = (t.astype(np.uint32) << 16).view(np.float32).astype(np.float64)
+        np.testing.assert_array_equal(f.sum(0), W.astype(np.float64))
+        assert np.all(np.abs(f[1]) <= np.abs(f[0]) * 2.0 ** -8 + 1e-45)
+        hi = (W.view(np.uint32) + 0x7FFF + ((W.view(np.uint32) >> 16) & 1)) >> 16
+        np.testing.assert_array_equal(t[0], hi.astype(np.uint16))
 
 
 def test_pack_rejects_wrong_state():

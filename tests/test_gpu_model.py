@@ -139,3 +139,24 @@ def test_cpu_input_raises(golden):
     model = make_model(golden, "cpu")
     with pytest.raises(SfaNativeError):
         model(torch.zeros(1, 3, 64, 64))
+
+
+@pytest.mark.parametrize("math", ["f32", "bf16x6"])
+def test_forward_608_math_modes(golden, gpu, math):
+    """Both convolution arithmetics (include/sfa_hip.h sfa_math) meet the logit bar on the
+    full-size frame; bf16x6 (default) is f32-accurate, not a reduced-precision mode."""
+    from data_process.kitti_bev_utils import makeBEVMap
+    from data_process.kitti_data_utils import get_filtered_lidar
+    from sfa_hip import _lib
+    model = make_model(golden, gpu)
+    eng = model._engine(gpu)
+    eng.set_math(_lib.MATH_F32 if math == "f32" else _lib.MATH_BF16X6)
+    assert _lib.lib().sfa_model_get_math(eng._h) == eng.math
+    cloud = synthetic.synthetic_point_cloud(1)
+    x = torch.from_numpy(makeBEVMap(get_filtered_lidar(cloud, gc.BOUNDARY), gc.BOUNDARY)[None])
+    with torch.no_grad():
+        out = model(x.to(gpu).float())
+    for h in gc.HEADS:
+        e = _err(out[h].cpu().numpy(), golden.model[f"e2e/{h}/full"])
+        print(f"{math} 608 {h}: max rel err {e:.3g}")
+        assert e <= TOL

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_kernel.h"
+#include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_x6_kernel.h"
 
 namespace sfa {
 void set_error(const char* fmt, ...) {
@@ -49,6 +50,37 @@ static float* dev_random(size_t n, unsigned seed, float scale) {
   return d;
 }
 
+static uint16_t bf16_rne(float f) {
+  unsigned u;
+  memcpy(&u, &f, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+static float bf16_f(uint16_t b) {
+  unsigned u = (unsigned)b << 16;
+  float f;
+  memcpy(&f, &u, 4);
+  return f;
+}
+// [N][Kpad] f32 (device) -> [3][N][Kpad] bf16 terms (device)
+static uint16_t* split_weights(const float* w, size_t n) {
+  std::vector<float> hw(n);
+  CK(hipMemcpy(hw.data(), w, n * 4, hipMemcpyDeviceToHost));
+  std::vector<uint16_t> hs(3 * n);
+  for (size_t i = 0; i < n; ++i) {
+    float x = hw[i];
+    for (int t = 0; t < 3; ++t) {
+      const uint16_t b = bf16_rne(x);
+      hs[t * n + i] = b;
+      x -= bf16_f(b);
+    }
+  }
+  uint16_t* d;
+  CK(hipMalloc(&d, hs.size() * 2));
+  CK(hipMemcpy(d, hs.data(), hs.size() * 2, hipMemcpyHostToDevice));
+  return d;
+}
+
 struct Shape {
   const char* name;
   int B, H, W, C, k, stride, pad, N;
@@ -67,6 +99,16 @@ struct Cand {
     #BM "x" #BN " w" #WM "x" #WN " bk" #BK " occ" #OCC " glds" #G " abl" #ABL, BK,        \
         [](const ConvArgs& a, hipStream_t s) { return launch_conv_cfg<BM, BN, WM, WN, BK, EPI, OCC, G, ABL>(a, s); } \
   }
+#define CANDX(BM, BN, WM, WN, BK, EPI, OCC)                                              \
+  Cand {                                                                                \
+    "x6 " #BM "x" #BN " w" #WM "x" #WN " bk" #BK " occ" #OCC, BK,                         \
+        [](const ConvArgs& a, hipStream_t s) { return launch_conv_x6_cfg<BM, BN, WM, WN, BK, EPI, OCC>(a, s); } \
+  }
+#define CANDXG(BM, BN, WM, EPI, OCC)                                                     \
+  Cand {                                                                                \
+    "x6g " #BM "x" #BN " w" #WM " occ" #OCC, 16,                                          \
+        [](const ConvArgs& a, hipStream_t s) { return launch_conv_x6g_cfg<BM, BN, WM, EPI, OCC>(a, s); } \
+  }
 #define CANDA(BM, BN, WM, WN, BK, EPI, OCC, ABL) CANDG(BM, BN, WM, WN, BK, EPI, OCC, false, ABL)
 #define CAND(BM, BN, WM, WN, BK, EPI, OCC) CANDA(BM, BN, WM, WN, BK, EPI, OCC, 0)
 
@@ -84,19 +126,21 @@ int main(int argc, char** argv) {
       {"head L0 3x3 256->5x64", 16, 76, 76, 256, 3, 1, 1, 320, true, false},
   };
   std::vector<Cand> n64 = {
-      CAND(128, 64, 32, 64, 16, EPI_STD, 4), CANDG(128, 64, 32, 64, 16, EPI_STD, 4, true, 0),
-      CANDG(128, 64, 32, 64, 16, EPI_STD, 3, true, 0), CANDG(256, 64, 64, 64, 16, EPI_STD, 2, true, 0),
-      CANDG(64, 64, 32, 32, 16, EPI_STD, 4, true, 0),
+      CAND(128, 64, 32, 64, 16, EPI_STD, 4),
+      CANDX(128, 64, 32, 64, 32, EPI_STD, 2),
+      CANDXG(128, 64, 32, EPI_STD, 2), CANDXG(256, 64, 32, EPI_STD, 1), CANDXG(256, 64, 64, EPI_STD, 1),
   };
   std::vector<Cand> nbig = {
-      CAND(64, 128, 32, 64, 16, EPI_STD, 4), CANDG(64, 128, 32, 64, 16, EPI_STD, 4, true, 0),
-      CANDG(128, 128, 64, 64, 16, EPI_STD, 2, true, 0), CANDG(64, 64, 32, 32, 16, EPI_STD, 4, true, 0),
-      CAND(64, 64, 32, 32, 32, EPI_STD, 4),
+      CAND(64, 128, 32, 64, 16, EPI_STD, 4),
+      CANDX(128, 128, 64, 64, 16, EPI_STD, 2), CANDX(64, 128, 32, 64, 32, EPI_STD, 2),
+      CANDXG(128, 128, 32, EPI_STD, 2), CANDXG(256, 128, 32, EPI_STD, 1), CANDXG(128, 256, 32, EPI_STD, 1),
+      CANDXG(256, 256, 32, EPI_STD, 1), CANDXG(64, 128, 32, EPI_STD, 2), CANDXG(64, 256, 32, EPI_STD, 1),
   };
   std::vector<Cand> heads = {
-      CAND(128, 64, 32, 64, 16, EPI_HEAD, 4), CANDG(128, 64, 32, 64, 16, EPI_HEAD, 4, true, 0),
-      CANDG(128, 64, 32, 64, 16, EPI_HEAD, 3, true, 0), CANDG(256, 64, 64, 64, 16, EPI_HEAD, 2, true, 0),
-      CANDG(64, 64, 32, 32, 16, EPI_HEAD, 4, true, 0),
+      CAND(128, 64, 32, 64, 16, EPI_HEAD, 4),
+      CANDX(128, 64, 32, 64, 32, EPI_HEAD, 2),
+      CANDXG(128, 320, 32, EPI_HEAD, 1), CANDXG(256, 320, 32, EPI_HEAD, 1),
+      CANDX(256, 320, 32, 320, 16, EPI_HEAD, 1), CANDXG(256, 64, 32, EPI_HEAD, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -168,6 +212,7 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(wv, hw2.data(), hw2.size() * 4, hipMemcpyHostToDevice));
       }
       a.w = wv;
+      a.wx = c.name.rfind("x6", 0) == 0 ? split_weights(wv, (size_t)sh.N * a.Kpad) : nullptr;
       a.y = y;
       a.hout = y;
       CK(hipMemset(y, 0, ysz * 4));
@@ -202,6 +247,7 @@ int main(int argc, char** argv) {
       printf("  %-32s %9.1f us  %7.1f TF/s  maxdiff %.2e (|ref| %.2e)\n", c.name.c_str(), med * 1e3,
              flop / (med * 1e-3) / 1e12, maxd, maxr);
       if (wv != w) CK(hipFree(wv));
+      if (a.wx) CK(hipFree(const_cast<uint16_t*>(a.wx)));
     }
     CK(hipFree(x));
     CK(hipFree(w));
