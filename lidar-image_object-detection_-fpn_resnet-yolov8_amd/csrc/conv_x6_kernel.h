@@ -22,6 +22,8 @@
 // conv_kernel.h) and split while it is written to LDS; W was split on the host.
 #pragma once
 
+#include <type_traits>
+
 #include "conv.h"
 
 namespace sfa {
@@ -308,34 +310,47 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_x6_kerne
   x6_epilogue<BM, BN, WM, WN, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wm, wn, tid);
 }
 
-// LDS-DMA variant: A (f32) and the three W terms (bf16) stream into a 3-deep ring with
-// buffer_load ... lds (no VGPR staging); A is split into its bf16 terms when a wave
-// reads its fragment.  Waves are stacked along M only (WN = BN), so every A element
-// is split exactly once.  BK = 16: an A row is 64 B (4 f32 quads, quad q of row R at
-// q ^ ((R >> 2) & 3)); a W-term row is 32 B (chunk c at c ^ ((R >> 3) & 1)).
+// LDS-DMA variant: A (f32) and the three W terms (bf16) stream into an NSTAGE-deep
+// ring with buffer_load ... lds (no VGPR staging); A is split into its bf16 terms when a
+// wave reads its fragment.  Waves are stacked along M only (WN = BN), so every A
+// element is split exactly once.  LDS images (16-B quad/chunk q of row R stored at
+// q ^ swz(R), conflict-free for the ds_read_b128 lane groups):
+//   A rows BK f32: 64 B (BK 16, swz = (R >> 2) & 3) or 128 B (BK 32, swz = (R >> 1) & 7)
+//   W rows BK bf16 per term: 32 B (BK 16, swz = (R >> 3) & 1) or 64 B (BK 32, (R >> 2) & 3)
 // DMA instructions (1 KiB each) are dealt round-robin to the waves; each wave waits for
 // its own with a counted vmcnt, then the barrier makes the whole stage visible.
-template <int BM, int BN, int WM, int EPI, int OCC>
+// ABL: diagnostic ablation bits for tools/convbench (0 in the product): 1 = no DMA in
+// the K loop, 2 = no A split (raw bits as terms), 4 = W fragments read once per k-step
+// group instead of per column block, 8 = no barrier.
+template <int BM, int BN, int WM, int EPI, int OCC, int BK = 16, int NSTAGE = 3, int ABL = 0>
 __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_x6g_kernel(const ConvArgs a) {
-  constexpr int BK = 16;
+  static_assert(BK == 16 || BK == 32, "BK");
+  static_assert(NSTAGE == 2 || NSTAGE == 3, "ring depth");
   constexpr int NW = BM / WM;
   constexpr int NT = NW * 64;
   constexpr int WN = BN;
   constexpr int TM = WM / 32, TN = WN / 32;
-  constexpr int A_BYTES = BM * 64, TERM_B = BN * 32;
+  constexpr int KST = BK / 16;
+  constexpr int AROW = BK * 4, BROW = BK * 2;         // bytes per LDS row
+  constexpr int A_BYTES = BM * AROW, TERM_B = BN * BROW;
   constexpr int STAGE = A_BYTES + 3 * TERM_B;
-  constexpr int ND_A = BM / 16;          // A DMA instructions per stage (16 rows each)
-  constexpr int ND_B = 3 * BN / 32;      // W DMA instructions per stage (32 rows each)
-  constexpr int ND = ND_A + ND_B;
+  constexpr int A_RPD = 1024 / AROW, B_RPD = 1024 / BROW;  // rows per DMA instruction
+  constexpr int ND_A = BM / A_RPD;
+  constexpr int ND_BT = BN / B_RPD;                         // per term
+  constexpr int ND = ND_A + 3 * ND_BT;
   constexpr int DPW = (ND + NW - 1) / NW;  // max per wave
   constexpr int DREM = ND % NW;            // waves < DREM issue DPW, the rest DPW - 1 (if DREM)
-  static_assert(BM % 16 == 0 && BN % 32 == 0, "tile");
+  static_assert(BM % A_RPD == 0 && BN % B_RPD == 0 && BN % 32 == 0, "tile");
   constexpr int HCH = BM < 128 ? BM : 128;
   constexpr int HEAD_BYTES = EPI == EPI_HEAD ? HCH * 65 * 4 : 0;
-  constexpr int LDS_BYTES = 3 * STAGE > HEAD_BYTES ? 3 * STAGE : HEAD_BYTES;
+  constexpr int LDS_BYTES = NSTAGE * STAGE > HEAD_BYTES ? NSTAGE * STAGE : HEAD_BYTES;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  auto swzA = [](int R) { return BK == 16 ? ((R >> 2) & 3) : ((R >> 1) & 7); };
+  auto swzB = [](int R) { return BK == 16 ? ((R >> 3) & 1) : ((R >> 2) & 3); };
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar DMA bookkeeping
   const int wm = wave, wn = 0;
   const int n_tiles = a.N / BN;
   const int lbid = xcd_remap(blockIdx.x, gridDim.x);
@@ -343,14 +358,19 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_x6g_kernel(const Con
   const int m0 = mt * BM, n0 = nt * BN;
   const int M = a.M;
 
-  // this wave's DMA instructions: d = wave + NW * i, i < DPW (d < ND)
+  // this wave's A DMA instructions: d = wave + NW * i (d < ND_A); lane -> row, quad
+  constexpr int QPR = AROW / 16;
+  const int arow_in = lane / QPR;
+  // logical f32 quad of this lane: the same for all of the wave's A instructions, since
+  // rows A_RPD*(wave + NW*i) + arow_in share swzA (BK 16: A_RPD = 16; BK 32: NW even)
+  static_assert(BK == 16 || NW % 2 == 0, "swizzle period");
+  const int kq = (lane % QPR) ^ swzA(A_RPD * wave + arow_in);
   constexpr int NSEG = 2;
   int r_ih[NSEG][DPW], r_iw[NSEG][DPW], r_pix[NSEG][DPW];
-  const int kq = (lane & 3) ^ ((lane >> 4) & 3);  // logical f32 quad of an A lane
 #pragma unroll
   for (int i = 0; i < DPW; ++i) {
     const int d = wave + NW * i;
-    const int R = 16 * d + (lane >> 2);          // A row (valid when d < ND_A)
+    const int R = A_RPD * d + arow_in;           // A row (valid when d < ND_A)
     const int m = m0 + R;
     const bool ok = d < ND_A && m < M;
     const int mm = ok ? m : 0;
@@ -376,12 +396,15 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_x6g_kernel(const Con
   const unsigned term_bytes = (unsigned)a.N * (unsigned)a.Kpad * 2u;
   const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<uint16_t*>(a.wx), (short)0, (int)(3u * term_bytes), 0x00020000);
+  // W lanes: row brow_in of the instruction's B_RPD rows, chunk (lane % CPR)
+  constexpr int CPR = BROW / 16;
+  const int brow_in = lane / CPR;
 
-  auto load_tile = [&](int kt, unsigned char* S) {
-    const int k0 = kt * BK;
-    const bool s1 = a.nseg > 1 && k0 >= a.kseg1;
-    const ConvSeg& g = s1 ? a.seg[1] : a.seg[0];
-    const int kl = s1 ? k0 - a.kseg1 : k0;
+  // A DMAs of one K-tile from segment SG (compile-time, so the buffer resource and
+  // the per-row window origins stay in SGPRs / VGPRs — no waterfall, no scratch)
+  auto load_a = [&](auto sgc, const __amdgpu_buffer_rsrc_t rs, int kl, unsigned char* S) {
+    constexpr int SG = decltype(sgc)::value;
+    const ConvSeg& g = a.seg[SG];
     const int kk = kl + 4 * kq;
     const int tap = kk >> g.logC;
     const int c = kk & (g.C - 1);
@@ -393,20 +416,31 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_x6g_kernel(const Con
     for (int i = 0; i < DPW; ++i) {
       const int d = wave + NW * i;
       if (d < ND_A) {
-        const int sg = s1 ? 1 : 0;
-        const int ih = sg ? r_ih[1][i] : r_ih[0][i];
-        const int iw = sg ? r_iw[1][i] : r_iw[0][i];
-        const int pix = sg ? r_pix[1][i] : r_pix[0][i];
-        const bool ok = tap_ok & ((unsigned)(ih + kh) < (unsigned)g.H) & ((unsigned)(iw + kw) < (unsigned)g.W);
-        const unsigned off = ok ? (unsigned)((((pix + toff) << g.logC) + c) << 2) : 0x80000000u;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(s1 ? rs1 : rs0, (__attribute__((address_space(3))) void*)(S + d * 1024), 16, off, 0, 0, 0);
-      } else if (d < ND) {
+        const bool ok = tap_ok & ((unsigned)(r_ih[SG][i] + kh) < (unsigned)g.H) &
+                        ((unsigned)(r_iw[SG][i] + kw) < (unsigned)g.W);
+        const unsigned off = ok ? (unsigned)((((r_pix[SG][i] + toff) << g.logC) + c) << 2) : 0x80000000u;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(S + d * 1024),
+                                                 16, off, 0, 0, 0);
+      }
+    }
+  };
+  auto load_tile = [&](int kt, unsigned char* S) {
+    const int k0 = kt * BK;
+    if (a.nseg > 1 && k0 >= a.kseg1)
+      load_a(std::integral_constant<int, 1>(), rs1, k0 - a.kseg1, S);
+    else
+      load_a(std::integral_constant<int, 0>(), rs0, k0, S);
+#pragma unroll
+    for (int i = 0; i < DPW; ++i) {
+      const int d = wave + NW * i;
+      if (d >= ND_A && d < ND) {
         const int e = d - ND_A;
-        const int t = e / (BN / 32);
-        const int R = (e % (BN / 32)) * 32 + (lane >> 1);
-        const int lc = (lane & 1) ^ ((R >> 3) & 1);
+        const int t = e / ND_BT;
+        const int R = (e % ND_BT) * B_RPD + brow_in;
+        const int lc = (lane % CPR) ^ swzB(R);
         const unsigned off = t * term_bytes + (unsigned)(((n0 + R) * a.Kpad + k0 + 8 * lc) << 1);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(S + A_BYTES + e * 1024), 16, off, 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsw, (__attribute__((address_space(3))) void*)(S + A_BYTES + e * 1024), 16, off, 0, 0, 0);
       }
     }
   };
@@ -422,62 +456,83 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_x6g_kernel(const Con
   const int r = lane & 31, h = lane >> 5;
   auto compute = [&](const unsigned char* S) {
     const unsigned char* SB = S + A_BYTES;
-    bf16x8_t af[3][TM];
 #pragma unroll
-    for (int mi = 0; mi < TM; ++mi) {
-      const int R = wm * WM + mi * 32 + r;
-      const int sw = (R >> 2) & 3;
-      const x6_f32x4 q0 = *reinterpret_cast<const x6_f32x4*>(S + R * 64 + (((2 * h) ^ sw) << 4));
-      const x6_f32x4 q1 = *reinterpret_cast<const x6_f32x4*>(S + R * 64 + (((2 * h + 1) ^ sw) << 4));
-      bf16x4_t t0, t1, t2, u0, u1, u2;
-      split3(q0, t0, t1, t2);
-      split3(q1, u0, u1, u2);
-      af[0][mi] = __builtin_shufflevector(t0, u0, 0, 1, 2, 3, 4, 5, 6, 7);
-      af[1][mi] = __builtin_shufflevector(t1, u1, 0, 1, 2, 3, 4, 5, 6, 7);
-      af[2][mi] = __builtin_shufflevector(t2, u2, 0, 1, 2, 3, 4, 5, 6, 7);
-    }
-#pragma unroll
-    for (int ni = 0; ni < TN; ++ni) {
-      const int R = ni * 32 + r;
-      const int byte = R * 32 + ((h ^ ((R >> 3) & 1)) << 4);
-      bf16x8_t b0 = *reinterpret_cast<const bf16x8_t*>(SB + byte);
-      bf16x8_t b1 = *reinterpret_cast<const bf16x8_t*>(SB + TERM_B + byte);
-      bf16x8_t b2 = *reinterpret_cast<const bf16x8_t*>(SB + 2 * TERM_B + byte);
+    for (int s = 0; s < KST; ++s) {
+      bf16x8_t af[3][TM];
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
-        x6_f32x16 c = acc[mi][ni];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][mi], b0, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][mi], b2, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][mi], b1, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][mi], b0, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][mi], b1, c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][mi], b0, c, 0, 0, 0);
-        acc[mi][ni] = c;
+        const int R = wm * WM + mi * 32 + r;
+        const int q = 4 * s + 2 * h;  // logical f32 quads q, q + 1 hold k = 16s + 8h .. + 7
+        const x6_f32x4 q0 = *reinterpret_cast<const x6_f32x4*>(S + R * AROW + ((q ^ swzA(R)) << 4));
+        const x6_f32x4 q1 = *reinterpret_cast<const x6_f32x4*>(S + R * AROW + (((q + 1) ^ swzA(R)) << 4));
+        if constexpr (ABL & 2) {
+          const bf16x8_t raw = __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(
+                                                               __builtin_bit_cast(x6_u32x4, q0), __builtin_bit_cast(x6_u32x4, q1), 0, 2, 4, 6));
+          af[0][mi] = raw;
+          af[1][mi] = raw;
+          af[2][mi] = raw;
+        } else {
+          bf16x4_t t0, t1, t2, u0, u1, u2;
+          split3(q0, t0, t1, t2);
+          split3(q1, u0, u1, u2);
+          af[0][mi] = __builtin_shufflevector(t0, u0, 0, 1, 2, 3, 4, 5, 6, 7);
+          af[1][mi] = __builtin_shufflevector(t1, u1, 0, 1, 2, 3, 4, 5, 6, 7);
+          af[2][mi] = __builtin_shufflevector(t2, u2, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+      }
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int R = ((ABL & 4) ? 0 : ni * 32) + r;
+        const int byte = R * BROW + (((2 * s + h) ^ swzB(R)) << 4);
+        bf16x8_t b0 = *reinterpret_cast<const bf16x8_t*>(SB + byte);
+        bf16x8_t b1 = *reinterpret_cast<const bf16x8_t*>(SB + TERM_B + byte);
+        bf16x8_t b2 = *reinterpret_cast<const bf16x8_t*>(SB + 2 * TERM_B + byte);
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) {
+          x6_f32x16 c = acc[mi][ni];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[2][mi], b0, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][mi], b2, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][mi], b1, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[1][mi], b0, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][mi], b1, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[0][mi], b0, c, 0, 0, 0);
+          acc[mi][ni] = c;
+        }
       }
     }
   };
 
   const int nk = a.Kpad / BK;
-  load_tile(0, smem);
-  load_tile(nk > 1 ? 1 : 0, smem + STAGE);
-  for (int kt = 0; kt < nk; ++kt) {
-    // this wave's DMAs of tile kt have landed (those of kt + 1 may be in flight)
-    if (DREM == 0 || wave < DREM)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW - 1) : "memory");
-    __builtin_amdgcn_s_barrier();  // ... and every wave's: stage kt % 3 is complete
-    load_tile(kt + 2 < nk ? kt + 2 : nk - 1, smem + ((kt + 2) % 3) * STAGE);
-    compute(smem + (kt % 3) * STAGE);
+  if constexpr (NSTAGE == 3) {
+    load_tile(0, smem);
+    load_tile(nk > 1 ? 1 : 0, smem + STAGE);
+    for (int kt = 0; kt < nk; ++kt) {
+      // this wave's DMAs of tile kt have landed (those of kt + 1 may be in flight)
+      if (DREM == 0 || wave < DREM)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW - 1) : "memory");
+      if constexpr (!(ABL & 8)) __builtin_amdgcn_s_barrier();  // ... and every wave's: stage kt % 3 is complete
+      if constexpr (!(ABL & 1)) load_tile(kt + 2 < nk ? kt + 2 : nk - 1, smem + ((kt + 2) % 3) * STAGE);
+      compute(smem + (kt % 3) * STAGE);
+    }
+  } else {
+    load_tile(0, smem);
+    for (int kt = 0; kt < nk; ++kt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt landed (this wave)
+      __builtin_amdgcn_s_barrier();  // every wave: stage kt & 1 complete, stage (kt+1) & 1 free
+      load_tile(kt + 1 < nk ? kt + 1 : nk - 1, smem + ((kt + 1) & 1) * STAGE);
+      compute(smem + (kt & 1) * STAGE);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   x6_epilogue<BM, BN, WM, WN, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wm, wn, tid);
 }
 
-template <int BM, int BN, int WM, int EPI, int OCC>
+template <int BM, int BN, int WM, int EPI, int OCC, int BK = 16, int NSTAGE = 3, int ABL = 0>
 inline int launch_conv_x6g_cfg(const ConvArgs& a, hipStream_t st) {
-  if (!a.wx || a.Kpad % 16 != 0 || (a.nseg == 2 && a.kseg1 % 16 != 0) || a.N % BN != 0) {
+  if (!a.wx || a.Kpad % BK != 0 || (a.nseg == 2 && a.kseg1 % BK != 0) || a.N % BN != 0) {
     set_error("conv_x6g: K/N not aligned to the tile or no split weights (Kpad=%d kseg1=%d N=%d)",
               a.Kpad, a.kseg1, a.N);
     return SFA_E_UNSUPPORTED;
@@ -491,7 +546,7 @@ inline int launch_conv_x6g_cfg(const ConvArgs& a, hipStream_t st) {
     set_error("conv_x6g: bad grid (M=%d N=%d)", a.M, a.N);
     return SFA_E_INVALID;
   }
-  hipLaunchKernelGGL((conv_x6g_kernel<BM, BN, WM, EPI, OCC>), dim3((unsigned)nblocks),
+  hipLaunchKernelGGL((conv_x6g_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, ABL>), dim3((unsigned)nblocks),
                      dim3((BM / WM) * 64), 0, st, a);
   SFA_LAUNCH_CHECK();
   return SFA_OK;

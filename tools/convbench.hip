@@ -109,6 +109,16 @@ struct Cand {
     "x6g " #BM "x" #BN " w" #WM " occ" #OCC, 16,                                          \
         [](const ConvArgs& a, hipStream_t s) { return launch_conv_x6g_cfg<BM, BN, WM, EPI, OCC>(a, s); } \
   }
+#define CANDXGK(BM, BN, WM, EPI, OCC, BK, NS)                                           \
+  Cand {                                                                                \
+    "x6g " #BM "x" #BN " w" #WM " occ" #OCC " bk" #BK " st" #NS, BK,                      \
+        [](const ConvArgs& a, hipStream_t s) { return launch_conv_x6g_cfg<BM, BN, WM, EPI, OCC, BK, NS>(a, s); } \
+  }
+#define CANDXGA(BM, BN, WM, EPI, OCC, ABL)                                               \
+  Cand {                                                                                \
+    "x6g " #BM "x" #BN " w" #WM " occ" #OCC " abl" #ABL, 16,                              \
+        [](const ConvArgs& a, hipStream_t s) { return launch_conv_x6g_cfg<BM, BN, WM, EPI, OCC, 16, 3, ABL>(a, s); } \
+  }
 #define CANDA(BM, BN, WM, WN, BK, EPI, OCC, ABL) CANDG(BM, BN, WM, WN, BK, EPI, OCC, false, ABL)
 #define CAND(BM, BN, WM, WN, BK, EPI, OCC) CANDA(BM, BN, WM, WN, BK, EPI, OCC, 0)
 
@@ -127,20 +137,16 @@ int main(int argc, char** argv) {
   };
   std::vector<Cand> n64 = {
       CAND(128, 64, 32, 64, 16, EPI_STD, 4),
-      CANDX(128, 64, 32, 64, 32, EPI_STD, 2),
-      CANDXG(128, 64, 32, EPI_STD, 2), CANDXG(256, 64, 32, EPI_STD, 1), CANDXG(256, 64, 64, EPI_STD, 1),
+      CANDXG(256, 64, 32, EPI_STD, 1), CANDXGA(256, 64, 32, EPI_STD, 1, 1), CANDXGA(256, 64, 32, EPI_STD, 1, 2),
+      CANDXGA(256, 64, 32, EPI_STD, 1, 4), CANDXGA(256, 64, 32, EPI_STD, 1, 8), CANDXGA(256, 64, 32, EPI_STD, 1, 15),
   };
   std::vector<Cand> nbig = {
       CAND(64, 128, 32, 64, 16, EPI_STD, 4),
-      CANDX(128, 128, 64, 64, 16, EPI_STD, 2), CANDX(64, 128, 32, 64, 32, EPI_STD, 2),
-      CANDXG(128, 128, 32, EPI_STD, 2), CANDXG(256, 128, 32, EPI_STD, 1), CANDXG(128, 256, 32, EPI_STD, 1),
-      CANDXG(256, 256, 32, EPI_STD, 1), CANDXG(64, 128, 32, EPI_STD, 2), CANDXG(64, 256, 32, EPI_STD, 1),
   };
   std::vector<Cand> heads = {
       CAND(128, 64, 32, 64, 16, EPI_HEAD, 4),
-      CANDX(128, 64, 32, 64, 32, EPI_HEAD, 2),
-      CANDXG(128, 320, 32, EPI_HEAD, 1), CANDXG(256, 320, 32, EPI_HEAD, 1),
-      CANDX(256, 320, 32, 320, 16, EPI_HEAD, 1), CANDXG(256, 64, 32, EPI_HEAD, 1),
+      CANDXG(256, 320, 32, EPI_HEAD, 1), CANDXGA(256, 320, 32, EPI_HEAD, 1, 1), CANDXGA(256, 320, 32, EPI_HEAD, 1, 2),
+      CANDXGA(256, 320, 32, EPI_HEAD, 1, 4), CANDXGA(256, 320, 32, EPI_HEAD, 1, 8), CANDXGA(256, 320, 32, EPI_HEAD, 1, 15),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
