@@ -137,16 +137,18 @@ int main(int argc, char** argv) {
   };
   std::vector<Cand> n64 = {
       CAND(128, 64, 32, 64, 16, EPI_STD, 4),
-      CANDXG(256, 64, 32, EPI_STD, 1), CANDXGA(256, 64, 32, EPI_STD, 1, 1), CANDXGA(256, 64, 32, EPI_STD, 1, 2),
-      CANDXGA(256, 64, 32, EPI_STD, 1, 4), CANDXGA(256, 64, 32, EPI_STD, 1, 8), CANDXGA(256, 64, 32, EPI_STD, 1, 15),
+      CANDXG(256, 64, 32, EPI_STD, 1), CANDXGK(128, 64, 32, EPI_STD, 2, 16, 2), CANDXGK(128, 64, 32, EPI_STD, 3, 16, 2),
+      CANDXGK(256, 64, 32, EPI_STD, 2, 16, 2),
   };
   std::vector<Cand> nbig = {
       CAND(64, 128, 32, 64, 16, EPI_STD, 4),
+      CANDXG(128, 128, 32, EPI_STD, 2), CANDXGK(128, 128, 32, EPI_STD, 2, 16, 2), CANDXGK(128, 256, 32, EPI_STD, 2, 16, 2),
+      CANDXGK(256, 128, 32, EPI_STD, 2, 16, 2),
   };
   std::vector<Cand> heads = {
       CAND(128, 64, 32, 64, 16, EPI_HEAD, 4),
-      CANDXG(256, 320, 32, EPI_HEAD, 1), CANDXGA(256, 320, 32, EPI_HEAD, 1, 1), CANDXGA(256, 320, 32, EPI_HEAD, 1, 2),
-      CANDXGA(256, 320, 32, EPI_HEAD, 1, 4), CANDXGA(256, 320, 32, EPI_HEAD, 1, 8), CANDXGA(256, 320, 32, EPI_HEAD, 1, 15),
+      CANDXG(256, 320, 32, EPI_HEAD, 1), CANDXGK(128, 320, 32, EPI_HEAD, 2, 16, 2),
+      CANDXGK(256, 320, 32, EPI_HEAD, 1, 16, 2),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
