@@ -54,12 +54,15 @@ const char* sfa_last_error_string(void);
  *                 SFA_BEV_NCHW3_F64  (B, 3, 608, 608) float64  (reference dtype)
  *                 SFA_BEV_NHWC4_F32  (B, 608, 608, 4) float32, channel 3 = 0
  *                                    (the model's input layout; no transpose)
+ *                 | SFA_BEV_FLIP_HW: the map is written flipped in both spatial
+ *                 dims (torch.flip(bev, [1, 2]), utils/demo_utils.py:110-111 — the
+ *                 back view of demo_2_sides.py with boundary_back)
  * scratch         device, sfa_bev_scratch_size(batch) bytes, ZERO on first use;
  *                 every call leaves it zeroed again.
  */
 #define SFA_BEV_MAX_BATCH 64
 enum sfa_bev_layout { SFA_BEV_NCHW3_F32 = 0, SFA_BEV_NCHW3_F64 = 1, SFA_BEV_NHWC4_F32 = 2 };
-enum sfa_bev_flags { SFA_BEV_RAW = 0, SFA_BEV_PREFILTERED = 1 };
+enum sfa_bev_flags { SFA_BEV_RAW = 0, SFA_BEV_PREFILTERED = 1, SFA_BEV_FLIP_HW = 2 };
 
 size_t sfa_bev_scratch_size(int batch);
 int sfa_bev_voxelize(const float* points, const int64_t* frame_offsets, int batch,
@@ -125,11 +128,13 @@ int sfa_model_set_math(sfa_model* model, int math);
 int sfa_model_get_math(const sfa_model* model);
 
 /* Forward.  x: device float32, layout SFA_IN_NCHW3 (B,3,H,W) as the reference
- * takes it, or SFA_IN_NHWC4 (B,H,W,4) as sfa_bev_voxelize writes it.
+ * takes it, SFA_IN_NHWC4 (B,H,W,4) as sfa_bev_voxelize writes it, or
+ * SFA_IN_NCHW3_FLIP_HW: (B,3,H,W) read as torch.flip(x, [2, 3]) — the back view of
+ * utils/demo_utils.py:110-111 do_detect, fused into the layout conversion.
  * H, W multiples of 32.  head_out[i]: device float32 (B, c_i, H/4, W/4) NCHW,
  * contiguous, forward head order — raw logits like the reference (no sigmoid).
  * workspace: sfa_forward_workspace_size(B, H, W) bytes. */
-enum sfa_input_layout { SFA_IN_NCHW3 = 0, SFA_IN_NHWC4 = 1 };
+enum sfa_input_layout { SFA_IN_NCHW3 = 0, SFA_IN_NHWC4 = 1, SFA_IN_NCHW3_FLIP_HW = 2 };
 size_t sfa_forward_workspace_size(const sfa_model* model, int batch, int height, int width);
 int sfa_model_forward(const sfa_model* model, const float* x, int in_layout, int batch, int height,
                       int width, float* const* head_out, void* workspace, size_t workspace_bytes,

@@ -9,12 +9,15 @@
 
 namespace sfa {
 
+// FLIP: torch.flip(x, [H, W]) fused in (utils/demo_utils.py:110-111, the back view):
+// pixel (h, w) of the output reads (H-1-h, W-1-w), i.e. flat index HW-1-p.
+template <bool FLIP>
 __global__ void __launch_bounds__(256) nchw3_to_nhwc4_kernel(const float* __restrict__ x,
                                                              float4* __restrict__ y, int B, int HW) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long long)B * HW) return;
   const int b = (int)(i / HW), p = (int)(i - (long long)b * HW);
-  const float* s = x + (size_t)b * 3 * HW + p;
+  const float* s = x + (size_t)b * 3 * HW + (FLIP ? HW - 1 - p : p);
   y[i] = make_float4(s[0], s[HW], s[2 * HW], 0.f);
 }
 
@@ -136,10 +139,14 @@ __global__ void __launch_bounds__(256) sigmoid_clamp_kernel(float* __restrict__ 
 
 static unsigned grid_of(long long n) { return (unsigned)((n + 255) / 256); }
 
-int launch_nchw3_to_nhwc4(const float* x, float* y, int B, int H, int W, hipStream_t st) {
+int launch_nchw3_to_nhwc4(const float* x, float* y, int B, int H, int W, bool flip, hipStream_t st) {
   const long long n = (long long)B * H * W;
-  hipLaunchKernelGGL(nchw3_to_nhwc4_kernel, dim3(grid_of(n)), dim3(256), 0, st, x,
-                     reinterpret_cast<float4*>(y), B, H * W);
+  if (flip)
+    hipLaunchKernelGGL(nchw3_to_nhwc4_kernel<true>, dim3(grid_of(n)), dim3(256), 0, st, x,
+                       reinterpret_cast<float4*>(y), B, H * W);
+  else
+    hipLaunchKernelGGL(nchw3_to_nhwc4_kernel<false>, dim3(grid_of(n)), dim3(256), 0, st, x,
+                       reinterpret_cast<float4*>(y), B, H * W);
   SFA_LAUNCH_CHECK();
   return SFA_OK;
 }

@@ -70,7 +70,7 @@ __global__ void __launch_bounds__(256) bev_scatter_kernel(const float4* __restri
   atomicAdd(counts + (size_t)b * kBevCells + cell, 1u);
 }
 
-template <int LAYOUT>
+template <int LAYOUT, bool FLIP>
 __global__ void __launch_bounds__(256) bev_gather_kernel(const float4* __restrict__ pts, BevArgs a,
                                                          unsigned long long* __restrict__ keys,
                                                          unsigned* __restrict__ counts,
@@ -92,16 +92,18 @@ __global__ void __launch_bounds__(256) bev_gather_kernel(const float4* __restric
     keys[sc] = 0ull;  // leave scratch zeroed for the next call
     counts[sc] = 0u;
   }
+  // torch.flip(bev, [1, 2]): cell (r, c) lands at (607 - r, 607 - c)
+  const int oc = FLIP ? kBevCells - 1 - cell : cell;
   if (LAYOUT == SFA_BEV_NHWC4_F32) {
     float4 v = make_float4(inten, height, (float)dens, 0.f);
-    reinterpret_cast<float4*>(out)[sc] = v;
+    reinterpret_cast<float4*>(out)[(size_t)b * kBevCells + oc] = v;
   } else if (LAYOUT == SFA_BEV_NCHW3_F32) {
-    float* o = reinterpret_cast<float*>(out) + (size_t)b * 3 * kBevCells + cell;
+    float* o = reinterpret_cast<float*>(out) + (size_t)b * 3 * kBevCells + oc;
     o[0] = inten;
     o[kBevCells] = height;
     o[2 * kBevCells] = (float)dens;
   } else {
-    double* o = reinterpret_cast<double*>(out) + (size_t)b * 3 * kBevCells + cell;
+    double* o = reinterpret_cast<double*>(out) + (size_t)b * 3 * kBevCells + oc;
     o[0] = (double)inten;
     o[kBevCells] = (double)height;
     o[2 * kBevCells] = dens;
@@ -125,7 +127,9 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
                 SFA_BEV_MAX_BATCH);
   SFA_CHECK_ARG(frame_offsets && boundary && out && scratch, "bev: null argument");
   SFA_CHECK_ARG(out_layout >= 0 && out_layout <= 2, "bev: bad out_layout %d", out_layout);
-  SFA_CHECK_ARG(flags == SFA_BEV_RAW || flags == SFA_BEV_PREFILTERED, "bev: bad flags %d", flags);
+  SFA_CHECK_ARG((flags & ~(SFA_BEV_PREFILTERED | SFA_BEV_FLIP_HW)) == 0, "bev: bad flags %d", flags);
+  const bool flip = (flags & SFA_BEV_FLIP_HW) != 0;
+  flags &= SFA_BEV_PREFILTERED;
   BevArgs a;
   int64_t max_n = 0;
   for (int b = 0; b <= batch; ++b) {
@@ -168,19 +172,19 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
     SFA_LAUNCH_CHECK();
   }
   dim3 g2((unsigned)ceil_div(kBevCells, 256), batch);
+#define SFA_BEV_GATHER(L, F) \
+  hipLaunchKernelGGL((bev_gather_kernel<L, F>), g2, dim3(256), 0, st, p4, a, keys, counts, out)
   switch (out_layout) {
     case SFA_BEV_NCHW3_F32:
-      hipLaunchKernelGGL(bev_gather_kernel<SFA_BEV_NCHW3_F32>, g2, dim3(256), 0, st, p4, a, keys,
-                         counts, out);
+      if (flip) SFA_BEV_GATHER(SFA_BEV_NCHW3_F32, true); else SFA_BEV_GATHER(SFA_BEV_NCHW3_F32, false);
       break;
     case SFA_BEV_NCHW3_F64:
-      hipLaunchKernelGGL(bev_gather_kernel<SFA_BEV_NCHW3_F64>, g2, dim3(256), 0, st, p4, a, keys,
-                         counts, out);
+      if (flip) SFA_BEV_GATHER(SFA_BEV_NCHW3_F64, true); else SFA_BEV_GATHER(SFA_BEV_NCHW3_F64, false);
       break;
     default:
-      hipLaunchKernelGGL(bev_gather_kernel<SFA_BEV_NHWC4_F32>, g2, dim3(256), 0, st, p4, a, keys,
-                         counts, out);
+      if (flip) SFA_BEV_GATHER(SFA_BEV_NHWC4_F32, true); else SFA_BEV_GATHER(SFA_BEV_NHWC4_F32, false);
   }
+#undef SFA_BEV_GATHER
   SFA_LAUNCH_CHECK();
   return SFA_OK;
 }

@@ -503,7 +503,9 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   SFA_CHECK_ARG(m && x && head_out && workspace, "forward: null argument");
   SFA_CHECK_ARG(B >= 1 && H >= 32 && W >= 32 && H % 32 == 0 && W % 32 == 0,
                 "forward: input (%d, 3, %d, %d) must have H, W multiples of 32", B, H, W);
-  SFA_CHECK_ARG(in_layout == SFA_IN_NCHW3 || in_layout == SFA_IN_NHWC4, "forward: bad layout");
+  SFA_CHECK_ARG(in_layout == SFA_IN_NCHW3 || in_layout == SFA_IN_NHWC4 ||
+                    in_layout == SFA_IN_NCHW3_FLIP_HW,
+                "forward: bad layout");
   SFA_CHECK_ARG((long long)B * H * W * 4 < (1ll << 31), "forward: input too large");
   const Bufs bf = plan_bufs(&m->arch, B, H, W);
   if (workspace_bytes < bf.total) {
@@ -518,8 +520,8 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   const Plan& p = m->plan;
 
   const float* xin = x;
-  if (in_layout == SFA_IN_NCHW3) {
-    SFA_RC(launch_nchw3_to_nhwc4(x, F(bf.xin), B, H, W, st));
+  if (in_layout != SFA_IN_NHWC4) {
+    SFA_RC(launch_nchw3_to_nhwc4(x, F(bf.xin), B, H, W, in_layout == SFA_IN_NCHW3_FLIP_HW, st));
     xin = F(bf.xin);
   }
   const int H2 = H / 2, W2 = W / 2;

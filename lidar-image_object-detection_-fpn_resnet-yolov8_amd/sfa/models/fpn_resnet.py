@@ -119,18 +119,25 @@ class PoseResNet(nn.Module):
         return eng
 
     def forward(self, x):
+        return self.forward_layout(x, _lib.IN_NCHW3)
+
+    def forward_layout(self, x, in_layout):
+        """forward() with the input read as ``in_layout``: _lib.IN_NCHW3 (the reference's), or
+        _lib.IN_NCHW3_FLIP_HW = forward(torch.flip(x, [2, 3])) with the flip fused in."""
         if not isinstance(x, torch.Tensor) or x.device.type != "cuda":
             raise _lib.SfaNativeError("PoseResNet.forward runs on the GPU (HIP) only; move the "
                                       "model input to a GPU device")
         if x.dim() != 4 or x.shape[1] != 3:
             raise ValueError(f"expected (B, 3, H, W), got {tuple(x.shape)}")
+        if in_layout not in (_lib.IN_NCHW3, _lib.IN_NCHW3_FLIP_HW):
+            raise ValueError(f"unsupported input layout {in_layout}")
         eng = self._engine(x.device)
         x = x.contiguous().float()
         with torch.no_grad(), torch.cuda.device(x.device):
             B, _, H, W = x.shape
             outs = eng.alloc_outputs(B, H, W)
             ws = eng.workspace(B, H, W)
-            eng.forward_into(x, outs, _lib.IN_NCHW3, ws)
+            eng.forward_into(x, outs, in_layout, ws)
             if self.capture_visualization:
                 self._capture(eng, ws, B, H, W)
             else:

@@ -23,8 +23,8 @@ SFA_OK = 0
 SFA_MAX_HEADS = 8
 SFA_BEV_MAX_BATCH = 64
 BEV_NCHW3_F32, BEV_NCHW3_F64, BEV_NHWC4_F32 = 0, 1, 2
-BEV_RAW, BEV_PREFILTERED = 0, 1
-IN_NCHW3, IN_NHWC4 = 0, 1
+BEV_RAW, BEV_PREFILTERED, BEV_FLIP_HW = 0, 1, 2
+IN_NCHW3, IN_NHWC4, IN_NCHW3_FLIP_HW = 0, 1, 2
 
 
 class SfaNativeError(RuntimeError):

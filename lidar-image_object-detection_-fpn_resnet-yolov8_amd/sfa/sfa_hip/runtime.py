@@ -16,6 +16,8 @@ from ._lib import SfaNativeError, check, lib
 
 DEFAULT_HEADS = {"hm_cen": 3, "cen_offset": 2, "direction": 2, "z_coor": 1, "dim": 3}
 DEFAULT_BOUNDARY = {"minX": 0, "maxX": 50, "minY": -25, "maxY": 25, "minZ": -2.73, "maxZ": 1.27}
+# config/kitti_config.py:35-42 boundary_back (demo_2_sides.py's rear view)
+DEFAULT_BOUNDARY_BACK = {"minX": -50, "maxX": 0, "minY": -25, "maxY": 25, "minZ": -2.73, "maxZ": 1.27}
 
 
 def _require_gpu_tensor(t: torch.Tensor, what: str, dtype=torch.float32) -> torch.Tensor:
@@ -104,7 +106,7 @@ class KfpnEngine:
 
     def forward_into(self, x: torch.Tensor, outs: dict, in_layout: int = _lib.IN_NCHW3,
                      workspace: torch.Tensor = None, stream: int = None) -> dict:
-        if in_layout == _lib.IN_NCHW3:
+        if in_layout != _lib.IN_NHWC4:
             B, C, H, W = x.shape
             if C != 3:
                 raise ValueError(f"expected (B, 3, H, W) input, got {tuple(x.shape)}")
@@ -146,7 +148,7 @@ class KfpnEngine:
 
     def forward(self, x: torch.Tensor, in_layout: int = _lib.IN_NCHW3) -> dict:
         x = _require_gpu_tensor(x, "PoseResNet.forward")
-        if in_layout == _lib.IN_NCHW3:
+        if in_layout != _lib.IN_NHWC4:
             B, _, H, W = x.shape
         else:
             B, H, W, _ = x.shape
@@ -291,21 +293,32 @@ class DetectorPipeline:
     """
 
     def __init__(self, engine: KfpnEngine, batch: int, height: int = 608, width: int = 608,
-                 K: int = 50, with_bev: bool = False, max_points: int = 0):
+                 K: int = 50, with_bev: bool = False, max_points: int = 0, two_sided: bool = False,
+                 boundary=DEFAULT_BOUNDARY, boundary_back=None):
+        """two_sided (with_bev only): every sweep is also voxelised with ``boundary_back``
+        and flipped (demo_2_sides.py: demo_dataset.py:70-88 + demo_utils.py:110-111), so one
+        run infers 2*batch maps: frames [0, batch) front, [batch, 2*batch) back."""
         self.engine = engine
         self.dev = engine.device
         self.B, self.H, self.W, self.K = batch, height, width, K
         self.with_bev = with_bev
+        self.two_sided = bool(two_sided)
+        if self.two_sided and not with_bev:
+            raise ValueError("two_sided needs with_bev (the back view is voxelised on the GPU)")
+        self.boundary = boundary
+        self.boundary_back = boundary_back if boundary_back is not None else DEFAULT_BOUNDARY_BACK
+        nmap = 2 * batch if self.two_sided else batch
+        self.nmap = nmap
         with torch.cuda.device(self.dev):
-            self.ws = engine.workspace(batch, height, width)
-            self.outs = engine.alloc_outputs(batch, height, width)
-            self.dets = torch.empty((batch, K, 10), dtype=torch.float32, device=self.dev)
-            self.dec_ws = _decoder.workspace(self.dev, batch, dict(engine.heads)["hm_cen"], K)
+            self.ws = engine.workspace(nmap, height, width)
+            self.outs = engine.alloc_outputs(nmap, height, width)
+            self.dets = torch.empty((nmap, K, 10), dtype=torch.float32, device=self.dev)
+            self.dec_ws = _decoder.workspace(self.dev, nmap, dict(engine.heads)["hm_cen"], K)
             if with_bev:
                 if (height, width) != (608, 608):
                     raise ValueError("the BEV grid is 608x608 (config/kitti_config.py:45-46)")
                 self.vox = BevVoxelizer(self.dev, batch)
-                self.bev = torch.empty((batch, 608, 608, 4), dtype=torch.float32, device=self.dev)
+                self.bev = torch.empty((nmap, 608, 608, 4), dtype=torch.float32, device=self.dev)
                 self.points = torch.zeros((max(max_points, 1), 4), dtype=torch.float32,
                                           device=self.dev)
                 self.offsets = np.zeros(batch + 1, np.int64)
@@ -327,8 +340,12 @@ class DetectorPipeline:
     def run(self):
         st = _lib.stream_ptr(self.dev)
         if self.with_bev:
-            self.vox(self.points, self.offsets, layout=_lib.BEV_NHWC4_F32, flags=_lib.BEV_RAW,
-                     out=self.bev, stream=st)
+            self.vox(self.points, self.offsets, boundary=self.boundary, layout=_lib.BEV_NHWC4_F32,
+                     flags=_lib.BEV_RAW, out=self.bev[: self.B], stream=st)
+            if self.two_sided:
+                self.vox(self.points, self.offsets, boundary=self.boundary_back,
+                         layout=_lib.BEV_NHWC4_F32, flags=_lib.BEV_RAW | _lib.BEV_FLIP_HW,
+                         out=self.bev[self.B:], stream=st)
             self.engine.forward_into(self.bev, self.outs, _lib.IN_NHWC4, self.ws, st)
         else:
             self.engine.forward_into(self.x, self.outs, _lib.IN_NCHW3, self.ws, st)

@@ -41,6 +41,12 @@ def golden_fusion():
 
 
 @pytest.fixture(scope="session")
+def golden_back():
+    import numpy as np
+    return np.load(os.path.join(GOLDEN, "back_golden.npz"))
+
+
+@pytest.fixture(scope="session")
 def golden_project():
     import numpy as np
     return np.load(os.path.join(GOLDEN, "project_golden.npz"))

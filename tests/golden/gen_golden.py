@@ -56,6 +56,13 @@ def _import_reference():
     for d in ("models", "utils", "config", "data_process"):
         shutil.copytree(os.path.join(REF, d), os.path.join(root, d),
                         ignore=shutil.ignore_patterns("__pycache__"))
+    # the reference's models/ has no __init__.py (a namespace package): a regular package
+    # of the same name anywhere on sys.path would win, so this repo's drop-in root must
+    # not be on the path while the reference is imported (sfa_hip stays cached)
+    sys.path[:] = [p for p in sys.path if os.path.abspath(p or ".") != os.path.abspath(PKG)]
+    for m in [m for m in sys.modules if m.split(".")[0] in ("models", "utils", "config",
+                                                             "data_process")]:
+        del sys.modules[m]
     cv2 = types.ModuleType("cv2")
     cv2.__dict__.update(dict(LINE_AA=16, FONT_HERSHEY_SIMPLEX=0))
     sys.modules["cv2"] = cv2
