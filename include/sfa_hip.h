@@ -234,6 +234,26 @@ int sfa_project_boxes(const double* real, const float* preds, const int32_t* off
                       int32_t* out_boxes, double* out_conf, int32_t* out_row, double* out_extent,
                       int32_t* out_offsets, void* stream);
 
+/* ------------------------------------------------------- .bin streaming --
+ * KITTI velodyne .bin files (data_process/kitti_dataset.py:119-122
+ * get_lidar = np.fromfile(path, float32).reshape(-1, 4)) read in batches by a producer
+ * thread with n_threads pread() workers into two host staging slots, overlapped with
+ * the GPU work of the previous batch.  pinned = 1: slots are hipHostMalloc'd and
+ * sfa_bin_stream_next copies a batch to DEVICE `points` with hipMemcpyAsync on
+ * `stream` (the slot is reused only after that copy completed); pinned = 0: plain host
+ * slots, `points` is a HOST buffer (memcpy; no device involved).  The stream allocates
+ * its own host memory (2 x max_points_per_batch x 16 B), never device memory.
+ * next() fills frame_offsets (HOST, batch + 1 entries, ready for sfa_bev_voxelize) and
+ * *n_frames (< batch for the last partial batch, 0 at the end).  A file whose float
+ * count is not a multiple of 4 fails the batch (the reference's reshape raises). */
+typedef struct sfa_bin_stream sfa_bin_stream;
+int sfa_bin_stream_create(const char* const* paths, int n_files, int batch,
+                          int64_t max_points_per_batch, int n_threads, int pinned,
+                          sfa_bin_stream** out);
+int sfa_bin_stream_next(sfa_bin_stream* s, float* points, int64_t capacity_points,
+                        int64_t* frame_offsets, int* n_frames, void* stream);
+void sfa_bin_stream_destroy(sfa_bin_stream* s);
+
 /* ------------------------------------------------------------ fusion --
  * Camera-LiDAR late fusion + NMS.  Replaces test6.py:310-348
  * create_fused_detections_wrapper -> :231-308 bayesian_inspired_fuse_overlapping_detections

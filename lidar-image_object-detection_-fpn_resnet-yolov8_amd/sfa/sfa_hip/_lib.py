@@ -128,6 +128,11 @@ _PROTOS["sfa_post_process"] = (_c_int, [_vp, _c_int, _c_int, ctypes.POINTER(SfaP
 _PROTOS["sfa_project_boxes"] = (_c_int, [_vp, _vp, _vp, _c_int, _vp,
                                          ctypes.POINTER(SfaProjectParams), _vp, _vp, _vp, _vp,
                                          _vp, _vp])
+_PROTOS["sfa_bin_stream_create"] = (_c_int, [ctypes.POINTER(ctypes.c_char_p), _c_int, _c_int, _c_i64,
+                                             _c_int, _c_int, ctypes.POINTER(_vp)])
+_PROTOS["sfa_bin_stream_next"] = (_c_int, [_vp, _vp, _c_i64, ctypes.POINTER(_c_i64),
+                                           ctypes.POINTER(_c_int), _vp])
+_PROTOS["sfa_bin_stream_destroy"] = (None, [_vp])
 EXPORTED_SYMBOLS = tuple(_PROTOS)
 
 _lib = None

@@ -337,7 +337,18 @@ class DetectorPipeline:
         self.points[: offs[-1]].copy_(host)
         self.offsets = offs
 
-    def run(self):
+    def load_points(self, points: torch.Tensor, offsets):
+        """Use a resident device buffer of points (e.g. a BinStream batch) without a copy;
+        a short batch is padded with empty frames."""
+        offs = np.asarray(offsets, dtype=np.int64)
+        if offs.size - 1 > self.B:
+            raise ValueError("more frames than the pipeline batch")
+        self.points = _require_gpu_tensor(points, "load_points")
+        self.offsets = np.concatenate([offs, np.full(self.B + 1 - offs.size, offs[-1], np.int64)])
+
+    def run(self, bev_done=None):
+        """Enqueue the step; ``bev_done`` (torch.cuda.Event) is recorded once the points have
+        been consumed (after voxelisation)."""
         st = _lib.stream_ptr(self.dev)
         if self.with_bev:
             self.vox(self.points, self.offsets, boundary=self.boundary, layout=_lib.BEV_NHWC4_F32,
@@ -346,6 +357,8 @@ class DetectorPipeline:
                 self.vox(self.points, self.offsets, boundary=self.boundary_back,
                          layout=_lib.BEV_NHWC4_F32, flags=_lib.BEV_RAW | _lib.BEV_FLIP_HW,
                          out=self.bev[self.B:], stream=st)
+            if bev_done is not None:
+                bev_done.record(torch.cuda.current_stream(self.dev))
             self.engine.forward_into(self.bev, self.outs, _lib.IN_NHWC4, self.ws, st)
         else:
             self.engine.forward_into(self.x, self.outs, _lib.IN_NCHW3, self.ws, st)

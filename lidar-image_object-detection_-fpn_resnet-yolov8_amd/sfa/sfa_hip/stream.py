@@ -1,0 +1,130 @@
+"""KITTI velodyne .bin streaming over sfa_bin_stream_* (include/sfa_hip.h).
+
+The reference reads one file per item (data_process/kitti_dataset.py:119-122 get_lidar:
+np.fromfile(path, float32).reshape(-1, 4)) and voxelises it on the CPU.  BinStream reads
+whole batches with a native reader pool into pinned staging memory and DMAs each batch into
+one resident device buffer, overlapped with the GPU work on the previous batch:
+
+    with BinStream(paths, batch=16, max_points_per_batch=16 * 150_000, device="cuda:0") as s:
+        for points, offsets in s:          # points: (N, 4) f32 on the GPU, offsets: np.int64
+            pipe.load_points(points, offsets)
+            dets = pipe.run()
+
+``device=None`` streams into host memory instead (no GPU needed; used by the CPU tests).
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib
+
+
+class BinStream:
+    def __init__(self, paths, batch: int, max_points_per_batch: int, n_threads: int = 8,
+                 device=None, n_buffers: int = 1):
+        self.paths = [str(p) for p in paths]
+        self.batch = int(batch)
+        self.cap = int(max_points_per_batch)
+        self.device = None if device is None else torch.device(device)
+        arr = (ctypes.c_char_p * max(1, len(self.paths)))(*[p.encode() for p in self.paths])
+        h = ctypes.c_void_p()
+        check(lib().sfa_bin_stream_create(arr, len(self.paths), self.batch, self.cap, int(n_threads),
+                                          0 if self.device is None else 1, ctypes.byref(h)),
+              "sfa_bin_stream_create")
+        self._h = h
+        # resident destination buffers, used in turn (2: the next batch can be copied while
+        # the previous one is still being voxelised)
+        self.bufs = [torch.empty((self.cap, 4), dtype=torch.float32,
+                                 device=self.device if self.device is not None else "cpu")
+                     for _ in range(max(1, int(n_buffers)))]
+        self.count = 0
+        self._offs = (ctypes.c_int64 * (self.batch + 1))()
+
+    def next(self, stream=None):
+        """-> (points (N, 4) view of the next resident buffer, offsets (n_frames + 1,)) or
+        None at the end.  Device mode: the copy is enqueued on ``stream``."""
+        n = ctypes.c_int()
+        st = None
+        if self.device is not None:
+            st = stream if stream is not None else _lib.stream_ptr(self.device)
+        buf = self.bufs[self.count % len(self.bufs)]
+        check(lib().sfa_bin_stream_next(self._h, buf.data_ptr(), self.cap, self._offs,
+                                        ctypes.byref(n), st), "sfa_bin_stream_next")
+        if n.value == 0:
+            return None
+        self.count += 1
+        offs = np.array(self._offs[: n.value + 1], dtype=np.int64)
+        return buf[: offs[-1]], offs
+
+    def __iter__(self):
+        while True:
+            item = self.next()
+            if item is None:
+                return
+            yield item
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().sfa_bin_stream_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class StreamingDetector:
+    """.bin files -> (pinned DMA) -> BEV -> KFPN forward -> decode, one batch at a time, with
+    the host reads and the H2D copy of batch k+1 overlapping the GPU work of batch k.
+
+    ``run(callback)`` calls ``callback(dets_view, n_frames, batch_index)`` after each batch
+    is enqueued (dets are valid once the current stream reaches that point)."""
+
+    def __init__(self, engine, paths, batch: int = 16, K: int = 50, n_threads: int = 8,
+                 max_points_per_frame: int = 200_000):
+        from .runtime import DetectorPipeline
+        self.dev = engine.device
+        self.batch = batch
+        self.pipe = DetectorPipeline(engine, batch, K=K, with_bev=True, max_points=1)
+        self.src = BinStream(paths, batch, batch * max_points_per_frame, n_threads, self.dev,
+                             n_buffers=2)
+
+    def run(self, callback=None):
+        with torch.cuda.device(self.dev):
+            comp = torch.cuda.current_stream()
+            copy = torch.cuda.Stream()
+            ev_copy = [torch.cuda.Event(), torch.cuda.Event()]
+            ev_bev = [torch.cuda.Event(), torch.cuda.Event()]
+            item = self.src.next(copy.cuda_stream)
+            ev_copy[0].record(copy)
+            k = 0
+            while item is not None:
+                pts, offs = item
+                comp.wait_event(ev_copy[k % 2])
+                self.pipe.load_points(pts, offs)
+                self.pipe.run(bev_done=ev_bev[k % 2])
+                if callback is not None:
+                    callback(self.pipe.dets, len(offs) - 1, k)
+                # the buffer of batch k-1 is free once its BEV pass is done
+                if k >= 1:
+                    copy.wait_event(ev_bev[(k + 1) % 2])
+                item = self.src.next(copy.cuda_stream)
+                ev_copy[(k + 1) % 2].record(copy)
+                k += 1
+            return k
+
+    def close(self):
+        self.src.close()
