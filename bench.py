@@ -52,9 +52,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--K", type=int, default=50)
-    ap.add_argument("--workload", choices=["bev_infer", "e2e", "stream"], default="bev_infer",
+    ap.add_argument("--workload", choices=["bev_infer", "e2e", "stream", "fusion"],
+                    default="bev_infer",
                     help="bev_infer: resident BEV frames (the headline); e2e: resident raw sweeps; "
-                         "stream: KITTI .bin files read + DMA'd per batch (SURVEY §8(f) #3)")
+                         "stream: KITTI .bin files read + DMA'd per batch (SURVEY §8(f) #3); "
+                         "fusion: BASELINE configs[4] chain up to camera-LiDAR fusion + NMS "
+                         "(use --batch 8)")
     ap.add_argument("--math", choices=["bf16x6", "f32"],
                     default="f32" if _lib.math_from_env() == _lib.MATH_F32 else "bf16x6",
                     help="convolution arithmetic (include/sfa_hip.h sfa_math; default bf16x6)")
@@ -233,10 +236,61 @@ def run_stream(args, rank, world, dev):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def run_fusion(args, rank, world, dev):
+    """BASELINE configs[4]: sweeps -> BEV -> forward -> decode -> post_process -> camera boxes
+    -> association / Bayesian fusion / NMS against camera boxes, all on the GPU in one HIP
+    graph (runtime.FusionPipeline).  The camera detector (YOLOv8n) is not in this framework:
+    its boxes are synthetic inputs, 30 per frame."""
+    import project_cases
+    from sfa_hip.runtime import FusionPipeline
+    arch = _lib.make_arch(DEFAULT_HEADS)
+    sd = synthetic.synthetic_state_dict(_lib.state_layout(arch), seed=0)
+    engine = KfpnEngine(arch, pack_state_dict(sd, arch), dev,
+                        math=_lib.MATH_F32 if args.math == "f32" else _lib.MATH_BF16X6)
+    cal = project_cases.calibs()["avg"]
+    calib = runtime_make_calib(cal)
+    clouds = [synthetic.synthetic_point_cloud(1000 * rank + i + 1) for i in range(args.batch)]
+    fp = FusionPipeline(engine, args.batch, [calib], K=args.K,
+                        max_points=sum(c.shape[0] for c in clouds), conf_source=_lib.CONF_SCORE)
+    fp.set_points(clouds)
+    cams = []
+    for i in range(args.batch):
+        u = synthetic.hash_uniform(77, i, 30 * 6).reshape(30, 6)
+        boxes = np.stack([u[:, 0] * 1150, u[:, 1] * 320, 10 + u[:, 2] * 120, 10 + u[:, 3] * 90], 1)
+        cams.append((boxes.astype(np.int64), u[:, 4].astype(np.float32).astype(np.float64),
+                     (u[:, 5] * 80).astype(np.int64)))
+    fp.set_camera(cams)
+    if not args.no_graph:
+        fp.capture()
+    for _ in range(args.warmup):
+        fp.replay()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        fp.replay()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def runtime_make_calib(c):
+    from sfa_hip.runtime import make_calib
+    return make_calib(c["V2C"], c["R0"], c["P2"], c["img_shape"])
+
+
 def main():
     args = parse()
     rank, world, dev = init_dist(args.gpus)
-    if args.workload == "stream":
+    if args.workload in ("stream", "fusion"):
+        if args.workload == "fusion":
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            elapsed, threads = run_fusion(args, rank, world, dev), None
+        else:
+            elapsed, threads = run_stream(args, rank, world, dev)
         elapsed, threads = run_stream(args, rank, world, dev)
         if world > 1:
             import torch.distributed as dist
@@ -246,17 +300,26 @@ def main():
             elapsed = float(t.item())
         if rank == 0:
             frames = world * args.batch * args.steps
+            if args.workload == "stream":
+                data = "synthetic 132,880-pt sweeps written as KITTI .bin files (page cache)"
+                cfg = {"workload": "KITTI .bin stream -> pinned DMA -> BEV -> fpn_resnet_18 "
+                                   "forward -> decode K=%d, bs=%d per GPU (no HIP graph: "
+                                   "per-batch frame offsets)" % (args.K, args.batch),
+                       "reader_threads": threads, "global_batch": world * args.batch}
+            else:
+                data = ("synthetic 132,880-pt sweeps + 30 synthetic camera boxes per frame "
+                        "(YOLOv8n itself not in the framework)")
+                cfg = {"workload": "BASELINE configs[4]: sweeps -> BEV -> fpn_resnet_18 forward -> "
+                                   "decode K=%d -> post_process -> camera boxes -> Bayesian "
+                                   "fusion + NMS, bs=%d per GPU, one HIP graph" % (args.K, args.batch),
+                       "global_batch": world * args.batch}
             print(json.dumps({
                 "metric": METRIC, "value": round(frames / elapsed, 2), "unit": "frames/s",
                 "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None,
                 "dtype": "f32 (bf16x6)" if args.math == "bf16x6" else "f32",
-                "data": "synthetic 132,880-pt sweeps written as KITTI .bin files (page cache)",
-                "config": {"workload": "KITTI .bin stream -> pinned DMA -> BEV -> fpn_resnet_18 "
-                                       "forward -> decode K=%d, bs=%d per GPU (no HIP graph: "
-                                       "per-batch frame offsets)" % (args.K, args.batch),
-                           "reader_threads": threads, "global_batch": world * args.batch},
+                "data": data, "config": cfg,
             }), flush=True)
         if world > 1:
             dist.destroy_process_group()

@@ -561,3 +561,134 @@ def project_boxes(real: torch.Tensor, offsets: torch.Tensor, calibs, preds=None,
                                   _lib.stream_ptr(dev)),
           "sfa_project_boxes")
     return boxes, conf, row, ext, off
+
+
+# ------------------------------------------------------- fused LiDAR + camera
+class FusionPipeline:
+    """BASELINE config #5 on one GPU (test6.py's per-frame flow, batched): sweeps -> BEV ->
+    KFPN forward -> decode (DetectorPipeline) -> post_process + convert_det_to_real_values
+    (sfa_post_process) -> camera boxes (sfa_project_boxes) -> association, fusion and NMS
+    with the camera detector's boxes (sfa_fuse_detections).  Every stage is a HIP kernel on
+    device-resident CSR buffers, so run() is one HIP-graph-capturable sequence.
+
+    The camera branch (YOLOv8n, ultralytics) is not part of this framework: its per-frame
+    boxes are inputs (``set_camera``), as test6.py:189-209 hands them to the fusion."""
+
+    def __init__(self, engine: KfpnEngine, batch: int, calibs, K: int = 50, max_points: int = 0,
+                 max_camera_boxes: int = 512, conf_threshold=0.3, fusion_iou_threshold=0.7,
+                 nms_threshold=0.5, mode=_lib.FUSE_BAYES, conf_source=_lib.CONF_CLASS_ID):
+        self.det = DetectorPipeline(engine, batch, K=K, with_bev=True, max_points=max_points)
+        self.B, self.K, self.dev = batch, K, engine.device
+        dev = self.dev
+        calibs = list(calibs)
+        self.calib = calib_tensor(calibs, dev)
+        self.conf_source = conf_source
+        self.params = _lib.SfaFusionParams(float(conf_threshold), float(fusion_iou_threshold),
+                                           float(nms_threshold), int(mode), 1)
+        self.proj_params = _lib.SfaProjectParams(0.3, int(conf_source),
+                                                 1 if len(calibs) == batch and batch > 1 else 0)
+        self.post_prm = post_params()
+        n = batch * K
+        f32, f64, i32 = torch.float32, torch.float64, torch.int32
+        with torch.cuda.device(dev):
+            self.preds = torch.empty((n, 8), dtype=f32, device=dev)
+            self.real = torch.empty((n, 8), dtype=f64, device=dev)
+            self.real_off = torch.zeros(batch + 1, dtype=i32, device=dev)
+            self.sboxes = torch.empty((n, 4), dtype=i32, device=dev)
+            self.sconf = torch.empty(n, dtype=f64, device=dev)
+            self.srow = torch.empty(n, dtype=i32, device=dev)
+            self.soff = torch.zeros(batch + 1, dtype=i32, device=dev)
+            cy = batch * max_camera_boxes
+            self.ybox = torch.zeros((cy, 4), dtype=i32, device=dev)
+            self.yconf = torch.zeros(cy, dtype=f64, device=dev)
+            self.ycls = torch.zeros(cy, dtype=i32, device=dev)
+            self.yoff = torch.zeros(batch + 1, dtype=i32, device=dev)
+            cap = cy + n
+            self.fbox = torch.empty((cap, 4), dtype=i32, device=dev)
+            self.fconf = torch.empty(cap, dtype=f64, device=dev)
+            self.fcls = torch.empty(cap, dtype=i32, device=dev)
+            self.fsrc = torch.empty(cap, dtype=i32, device=dev)
+            self.fcount = torch.empty(batch, dtype=i32, device=dev)
+            self.fkeep = torch.empty(cap, dtype=i32, device=dev)
+            self.fkeep_count = torch.empty(batch, dtype=i32, device=dev)
+        self.max_camera_boxes = max_camera_boxes
+        self.graph = None
+
+    def set_points(self, clouds):
+        self.det.set_points(clouds)
+
+    def set_camera(self, frames):
+        """frames: per frame (boxes (n, 4) int [x, y, w, h], conf (n,), class ids (n,))."""
+        if len(frames) != self.B:
+            raise ValueError("one camera detection list per frame")
+        b, c, k, off = [], [], [], [0]
+        for boxes, conf, cls in frames:
+            boxes = np.asarray(boxes, np.int32).reshape(-1, 4)
+            if boxes.shape[0] > min(512, self.max_camera_boxes):
+                raise ValueError("at most 512 camera boxes per frame")
+            b.append(boxes)
+            c.append(np.asarray(conf, np.float64).reshape(-1))
+            k.append(np.asarray(cls, np.int32).reshape(-1))
+            off.append(off[-1] + boxes.shape[0])
+        n = off[-1]
+        if n:
+            self.ybox[:n].copy_(torch.from_numpy(np.concatenate(b)))
+            self.yconf[:n].copy_(torch.from_numpy(np.concatenate(c)))
+            self.ycls[:n].copy_(torch.from_numpy(np.concatenate(k)))
+        self.yoff.copy_(torch.tensor(off, dtype=torch.int32))
+
+    def run(self):
+        st = _lib.stream_ptr(self.dev)
+        L = lib()
+        dets = self.det.run()
+        check(L.sfa_post_process(dets.data_ptr(), self.B, self.K, ctypes.byref(self.post_prm),
+                                 self.preds.data_ptr(), self.real.data_ptr(),
+                                 self.real_off.data_ptr(), st), "sfa_post_process")
+        check(L.sfa_project_boxes(self.real.data_ptr(), self.preds.data_ptr(),
+                                  self.real_off.data_ptr(), self.B, self.calib.data_ptr(),
+                                  ctypes.byref(self.proj_params), self.sboxes.data_ptr(),
+                                  self.sconf.data_ptr(), self.srow.data_ptr(), None,
+                                  self.soff.data_ptr(), st), "sfa_project_boxes")
+        check(L.sfa_fuse_detections(self.B, self.ybox.data_ptr(), self.yconf.data_ptr(),
+                                    self.ycls.data_ptr(), self.yoff.data_ptr(),
+                                    self.sboxes.data_ptr(), self.sconf.data_ptr(),
+                                    self.soff.data_ptr(), ctypes.byref(self.params),
+                                    self.fbox.data_ptr(), self.fconf.data_ptr(),
+                                    self.fcls.data_ptr(), self.fsrc.data_ptr(), None, None,
+                                    self.fcount.data_ptr(), self.fkeep.data_ptr(),
+                                    self.fkeep_count.data_ptr(), st), "sfa_fuse_detections")
+        return self.fcount
+
+    def capture(self):
+        with torch.cuda.device(self.dev):
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self.run()
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self.run()
+            self.graph = g
+        return g
+
+    def replay(self):
+        if self.graph is None:
+            return self.run()
+        self.graph.replay()
+        return self.fcount
+
+    def results(self):
+        """Host copy per frame: (fused boxes, conf, cls, source, NMS keep indices)."""
+        yoff = self.yoff.cpu().numpy()
+        soff = self.soff.cpu().numpy()
+        cnt, kc = self.fcount.cpu().numpy(), self.fkeep_count.cpu().numpy()
+        fb, fc, fk, fs, keep = (t.cpu().numpy() for t in (self.fbox, self.fconf, self.fcls,
+                                                          self.fsrc, self.fkeep))
+        out = []
+        for b in range(self.B):
+            base = yoff[b] + soff[b]
+            n = int(cnt[b])
+            out.append((fb[base:base + n], fc[base:base + n], fk[base:base + n], fs[base:base + n],
+                        keep[base:base + int(kc[b])]))
+        return out
