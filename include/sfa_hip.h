@@ -112,7 +112,12 @@ size_t sfa_packed_floats(const sfa_arch* arch);
 int sfa_pack_weights(const sfa_arch* arch, const float* state, size_t state_floats, float* packed);
 
 /* A model handle references a device copy of the packed weights (caller-owned,
- * must outlive the handle).  No device memory is allocated. */
+ * must outlive the handle).  No device memory is allocated.  The handle owns one side
+ * stream + two events on the device current at creation: a forward on a stream of that
+ * device runs the level-0 detection heads on the side stream, overlapping the rest of the
+ * FPN and the level-1/2 heads (forked/joined by events, so HIP-graph capture of the
+ * caller's stream records both branches); on another device everything stays on the
+ * caller's stream. */
 typedef struct sfa_model sfa_model;
 int sfa_model_create(const sfa_arch* arch, const float* packed_device, sfa_model** out);
 void sfa_model_destroy(sfa_model* model);

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -248,6 +249,13 @@ struct sfa_model {
   const float* w;
   Plan plan;
   int math;
+  // Side stream for the level-0 heads (they only need up_level2, so they overlap the rest
+  // of the FPN and the level-1/2 heads); created with the model on the current device,
+  // used only when the forward's stream is on that device.
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  int device = -1;
+  std::mutex fork_mu;  // fork ... join of one forward is not interleaved with another's
 };
 
 extern "C" int sfa_abi_version(void) { return SFA_ABI_VERSION; }
@@ -383,11 +391,25 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   m->w = packed_device;
   m->plan = make_plan(arch);
   m->math = SFA_MATH_BF16X6;
+  if (hipGetDevice(&m->device) != hipSuccess ||
+      hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&m->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&m->join, hipEventDisableTiming) != hipSuccess) {
+    // no device (or no stream): the forward runs every launch on the caller's stream
+    (void)hipGetLastError();
+    m->side = nullptr;
+  }
   *out = m;
   return SFA_OK;
 }
 
-extern "C" void sfa_model_destroy(sfa_model* model) { delete model; }
+extern "C" void sfa_model_destroy(sfa_model* model) {
+  if (!model) return;
+  if (model->fork) (void)hipEventDestroy(model->fork);
+  if (model->join) (void)hipEventDestroy(model->join);
+  if (model->side) (void)hipStreamDestroy(model->side);
+  delete model;
+}
 
 extern "C" int sfa_model_set_math(sfa_model* model, int math) {
   SFA_CHECK_ARG(model, "set_math: null model");
@@ -587,23 +609,6 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     SFA_RC(launch_conv(a, EPI_STD, m->math, st));
   }
   SFA_RC(launch_upsample2x(F(bf.c1), F(bf.up2), B, H16, W16, 256, st));
-  {
-    ConvArgs a = conv_args(wb, p.fpn[1], B, H8, W8, F(bf.c2), nullptr, 0);
-    a.nseg = 2;
-    a.kseg1 = 256;
-    a.seg[0] = seg(F(bf.up2), B, H8, W8, 256, 1, 1, 0);
-    a.seg[1] = seg(F(bf.l[1]), B, H8, W8, 128, 1, 1, 0);
-    SFA_RC(launch_conv(a, EPI_STD, m->math, st));
-  }
-  SFA_RC(launch_upsample2x(F(bf.c2), F(bf.up3), B, H8, W8, 128, st));
-  {
-    ConvArgs a = conv_args(wb, p.fpn[2], B, H4, W4, F(bf.up4), nullptr, 0);
-    a.nseg = 2;
-    a.kseg1 = 128;
-    a.seg[0] = seg(F(bf.up3), B, H4, W4, 128, 1, 1, 0);
-    a.seg[1] = seg(F(bf.l[0]), B, H4, W4, 64, 1, 1, 0);
-    SFA_RC(launch_conv(a, EPI_STD, m->math, st));
-  }
   // Detection heads (fpn_resnet.py:219-233): per level all heads in one launch,
   // conv3x3 -> ReLU -> conv1x1 fused; channel-planar level outputs.
   int hoff[SFA_MAX_HEADS] = {0};
@@ -615,7 +620,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   const float* lin[3] = {F(bf.up2), F(bf.up3), F(bf.up4)};
   const int lh[3] = {H8, H4, H4}, lw[3] = {W8, W4, W4};
   float* lout[3] = {F(bf.L0), F(bf.L1), F(bf.L2)};
-  for (int f = 0; f < 3; ++f) {
+  auto launch_head = [&](int f, hipStream_t hs) {
     const PHeads& hp = p.heads[f];
     ConvArgs a;
     memset(&a, 0, sizeof a);
@@ -637,8 +642,42 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       a.hoff[j] = hoff[j];
     }
     a.hout = lout[f];
-    SFA_RC(launch_conv(a, EPI_HEAD, m->math, st));
+    return launch_conv(a, EPI_HEAD, m->math, hs);
+  };
+  // level 0 needs only up_level2: fork it onto the side stream (graph capture follows
+  // the event edges), join before apply_kfpn
+  int sdev = -1;
+  const bool overlap = m->side && hipStreamGetDevice(st, &sdev) == hipSuccess && sdev == m->device;
+  std::unique_lock<std::mutex> fork_lock(const_cast<sfa_model*>(m)->fork_mu, std::defer_lock);
+  if (overlap) {
+    fork_lock.lock();
+    SFA_HIP_TRY(hipEventRecord(m->fork, st));
+    SFA_HIP_TRY(hipStreamWaitEvent(m->side, m->fork, 0));
+    SFA_RC(launch_head(0, m->side));
+    SFA_HIP_TRY(hipEventRecord(m->join, m->side));
+  } else {
+    SFA_RC(launch_head(0, st));
   }
+  {
+    ConvArgs a = conv_args(wb, p.fpn[1], B, H8, W8, F(bf.c2), nullptr, 0);
+    a.nseg = 2;
+    a.kseg1 = 256;
+    a.seg[0] = seg(F(bf.up2), B, H8, W8, 256, 1, 1, 0);
+    a.seg[1] = seg(F(bf.l[1]), B, H8, W8, 128, 1, 1, 0);
+    SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+  }
+  SFA_RC(launch_upsample2x(F(bf.c2), F(bf.up3), B, H8, W8, 128, st));
+  {
+    ConvArgs a = conv_args(wb, p.fpn[2], B, H4, W4, F(bf.up4), nullptr, 0);
+    a.nseg = 2;
+    a.kseg1 = 128;
+    a.seg[0] = seg(F(bf.up3), B, H4, W4, 128, 1, 1, 0);
+    a.seg[1] = seg(F(bf.l[0]), B, H4, W4, 64, 1, 1, 0);
+    SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+  }
+  SFA_RC(launch_head(1, st));
+  SFA_RC(launch_head(2, st));
+  if (overlap) SFA_HIP_TRY(hipStreamWaitEvent(st, m->join, 0));
   // apply_kfpn (fpn_resnet.py:248-254)
   KfpnOut ko;
   memset(&ko, 0, sizeof ko);

@@ -71,8 +71,9 @@ class KfpnEngine:
                       for j in range(arch.num_heads)]
         self.weights = torch.from_numpy(packed_host).to(self.device)
         h = ctypes.c_void_p()
-        check(lib().sfa_model_create(ctypes.byref(arch), self.weights.data_ptr(), ctypes.byref(h)),
-              "sfa_model_create")
+        with torch.cuda.device(self.device):  # the model's side stream lives on this device
+            check(lib().sfa_model_create(ctypes.byref(arch), self.weights.data_ptr(), ctypes.byref(h)),
+                  "sfa_model_create")
         self._h = h
         self._ws = {}
         self.set_math(_lib.math_from_env() if math is None else math)
