@@ -62,6 +62,9 @@ def parse():
                     default="f32" if _lib.math_from_env() == _lib.MATH_F32 else "bf16x6",
                     help="convolution arithmetic (include/sfa_hip.h sfa_math; default bf16x6)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="steps in flight on separate streams (each with its own buffers and "
+                         "model handle); >1 lets one step's kernel tails overlap the next's")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=4, help="frames timed for the CPU baseline")
     return ap.parse_args()
@@ -324,41 +327,51 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    pipe = build_pipeline(dev, args, rank)
-    steps = StepGraphs(pipe, not args.no_graph)
+    nf = max(1, args.inflight)
+    pipes = [build_pipeline(dev, args, rank) for _ in range(nf)]
+    steps = [StepGraphs(p, not args.no_graph) for p in pipes]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nf - 1)]
     gather = world > 1
     if gather:
         import torch.distributed as dist
         from sfa_hip import dist as sdist
         frame_ids = torch.arange(rank * args.batch, (rank + 1) * args.batch, device=dev)
 
-    def one_step():
-        steps.run(0)
-        steps.run(1)
-        if gather:
-            sdist.gather_detections(pipe.dets, frame_ids)
+    def one_step(k, ev=None):
+        i = k % nf
+        with torch.cuda.stream(streams[i]):
+            if ev is not None:
+                ev[0].record()
+            steps[i].run(0)
+            if ev is not None:
+                ev[1].record()
+            steps[i].run(1)
+            if ev is not None:
+                ev[2].record()
+            if gather:
+                sdist.gather_detections(pipes[i].dets, frame_ids)
 
-    for _ in range(args.warmup):
-        one_step()
+    for k in range(args.warmup):
+        one_step(k)
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        ev[k][0].record(stream)
-        steps.run(0)
-        ev[k][1].record(stream)
-        steps.run(1)
-        ev[k][2].record(stream)
-        if gather:
-            sdist.gather_detections(pipe.dets, frame_ids)
+        one_step(k, ev[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if nf > 1:
+        # per-stage times with one step in flight (the in-flight events overlap): a short
+        # untimed-for-value pass on stream 0 only, for the roofline and stages_ms
+        torch.cuda.synchronize()
+        for k in range(args.steps):
+            one_step(k * nf, ev[k])
+        torch.cuda.synchronize()
     fwd_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     if world > 1:
@@ -370,6 +383,7 @@ def main():
     value = frames / elapsed
     if rank == 0:
         flop_step = CONV_FLOP_PER_FRAME * args.batch
+        # the forward's own event time with one step in flight (the conv launches + aux)
         achieved = flop_step / (fwd_ms * 1e-3) / 1e12
         x6 = args.math == "bf16x6"
         peak = PEAK_BF16X6_TFLOPS if x6 else PEAK_FP32_MFMA_TFLOPS
@@ -399,8 +413,10 @@ def main():
                 "input": "3x608x608",
                 "parallelism": f"dp{world} (frame-sharded replicas; RCCL all_gather of detections)",
                 "hip_graph": not args.no_graph,
+                "steps_in_flight": nf,
             },
-            "stages_ms": {"forward": round(fwd_ms, 4), "decode": round(dec_ms, 4)},
+            "stages_ms": {"forward": round(fwd_ms, 4), "decode": round(dec_ms, 4),
+                          "note": "one step in flight; value/ms_per_step use %d in flight" % nf},
             "roofline": {
                 "bound": "mfma",
                 "kernel": ("conv_x6_kernel / conv_x6g_kernel" if x6 else "conv_mfma_kernel") +
