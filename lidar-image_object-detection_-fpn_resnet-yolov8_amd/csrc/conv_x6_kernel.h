@@ -322,13 +322,15 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_x6_kerne
 // ABL: diagnostic ablation bits for tools/convbench (0 in the product): 1 = no DMA in
 // the K loop, 2 = no A split (raw bits as terms), 4 = W fragments read once per k-step
 // group instead of per column block, 8 = no barrier.
-template <int BM, int BN, int WM, int EPI, int OCC, int BK = 16, int NSTAGE = 3, int ABL = 0>
-__global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_x6g_kernel(const ConvArgs a) {
+template <int BM, int BN, int WM, int EPI, int OCC, int BK = 16, int NSTAGE = 3, int ABL = 0,
+          int WNT = BN>
+__global__ void __launch_bounds__((BM / WM) * (BN / WNT) * 64, OCC) conv_x6g_kernel(const ConvArgs a) {
   static_assert(BK == 16 || BK == 32, "BK");
   static_assert(NSTAGE == 2 || NSTAGE == 3, "ring depth");
-  constexpr int NW = BM / WM;
+  constexpr int WN = WNT;                 // BN: waves along M only (A split once)
+  constexpr int WAVES_N = BN / WN;
+  constexpr int NW = (BM / WM) * WAVES_N;
   constexpr int NT = NW * 64;
-  constexpr int WN = BN;
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int KST = BK / 16;
   constexpr int AROW = BK * 4, BROW = BK * 2;         // bytes per LDS row
@@ -351,7 +353,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_x6g_kernel(const Con
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: scalar DMA bookkeeping
-  const int wm = wave, wn = 0;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int n_tiles = a.N / BN;
   const int lbid = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = lbid / n_tiles, nt = lbid - mt * n_tiles;
@@ -482,7 +484,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_x6g_kernel(const Con
       }
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
-        const int R = ((ABL & 4) ? 0 : ni * 32) + r;
+        const int R = ((ABL & 4) ? 0 : wn * WN + ni * 32) + r;
         const int byte = R * BROW + (((2 * s + h) ^ swzB(R)) << 4);
         bf16x8_t b0 = *reinterpret_cast<const bf16x8_t*>(SB + byte);
         bf16x8_t b1 = *reinterpret_cast<const bf16x8_t*>(SB + TERM_B + byte);
@@ -530,7 +532,8 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_x6g_kernel(const Con
   x6_epilogue<BM, BN, WM, WN, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wm, wn, tid);
 }
 
-template <int BM, int BN, int WM, int EPI, int OCC, int BK = 16, int NSTAGE = 3, int ABL = 0>
+template <int BM, int BN, int WM, int EPI, int OCC, int BK = 16, int NSTAGE = 3, int ABL = 0,
+          int WNT = BN>
 inline int launch_conv_x6g_cfg(const ConvArgs& a, hipStream_t st) {
   if (!a.wx || a.Kpad % BK != 0 || (a.nseg == 2 && a.kseg1 % BK != 0) || a.N % BN != 0) {
     set_error("conv_x6g: K/N not aligned to the tile or no split weights (Kpad=%d kseg1=%d N=%d)",
@@ -546,8 +549,8 @@ inline int launch_conv_x6g_cfg(const ConvArgs& a, hipStream_t st) {
     set_error("conv_x6g: bad grid (M=%d N=%d)", a.M, a.N);
     return SFA_E_INVALID;
   }
-  hipLaunchKernelGGL((conv_x6g_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, ABL>), dim3((unsigned)nblocks),
-                     dim3((BM / WM) * 64), 0, st, a);
+  hipLaunchKernelGGL((conv_x6g_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, ABL, WNT>),
+                     dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WNT) * 64), 0, st, a);
   SFA_LAUNCH_CHECK();
   return SFA_OK;
 }
