@@ -337,9 +337,19 @@ def main():
         from sfa_hip import dist as sdist
         frame_ids = torch.arange(rank * args.batch, (rank + 1) * args.batch, device=dev)
 
+    if gather:
+        # all-gathers go on one stream in step order (the same collective order on every
+        # rank); a pipeline's detections are overwritten only after their gather finished
+        comm = torch.cuda.Stream()
+        step_done = [torch.cuda.Event() for _ in range(nf)]
+        comm_done = [torch.cuda.Event() for _ in range(nf)]
+        gathered = [0] * nf
+
     def one_step(k, ev=None):
         i = k % nf
         with torch.cuda.stream(streams[i]):
+            if gather and gathered[i]:
+                streams[i].wait_event(comm_done[i])
             if ev is not None:
                 ev[0].record()
             steps[i].run(0)
@@ -349,7 +359,13 @@ def main():
             if ev is not None:
                 ev[2].record()
             if gather:
+                step_done[i].record()
+        if gather:
+            with torch.cuda.stream(comm):
+                comm.wait_event(step_done[i])
                 sdist.gather_detections(pipes[i].dets, frame_ids)
+                comm_done[i].record()
+            gathered[i] = 1
 
     for k in range(args.warmup):
         one_step(k)

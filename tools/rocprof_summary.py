@@ -52,6 +52,16 @@ def main():
     for k, d in sorted(by_kernel.items(), key=lambda kv: -sum(kv[1])):
         print(f"{k:90s} {len(d):6d} {sum(d) / len(d) / 1e3:10.2f} {sum(d) / 1e6:10.3f} "
               f"{100 * sum(d) / total:6.2f}")
+    # per forward: a forward starts at each kfpn-input conversion / stem launch and ends
+    # at kfpn_combine; conv = every implicit-GEMM launch
+    fwd = [r for r in rows if "kfpn_combine" in r["name"]]
+    if fwd:
+        nf = len(fwd)
+        conv = sum(r["dur"] for r in rows if re.search(r"conv_(mfma|x6g?)_kernel", r["name"]))
+        aux = sum(r["dur"] for r in rows if re.search(r"maxpool|upsample|nchw3|kfpn", r["name"]))
+        print(f"# forwards: {nf}; per forward: conv launches {conv / nf / 1e3:.1f} us, "
+              f"maxpool/upsample/layout/kfpn {aux / nf / 1e3:.1f} us "
+              f"(durations summed; concurrent launches overlap in wall time)")
     print("\n# per launch shape (grid = total work-items)")
     print(f"{'kernel':90s} {'grid':>22s} {'calls':>6s} {'avg_us':>10s}")
     for (k, g), d in sorted(by_shape.items(), key=lambda kv: -sum(kv[1])):
