@@ -2,8 +2,8 @@
 """Benchmark of the MI355X hot path — BEV frames/s at 608x608, bs=16 per GPU.
 
 One step = one batch of 16 synthetic 3x608x608 BEV frames, resident in HBM,
-through the KFPN FPN-ResNet-18 forward (23 implicit-GEMM conv launches — bf16x6
-split-operand MFMA by default, ``--math f32`` for the f32 MFMA kernels — + maxpool /
+through the KFPN FPN-ResNet-18 forward (23 implicit-GEMM conv launches — split-operand
+MFMA, ``--math fp16x3|bf16x6|f32`` (include/sfa_hip.h sfa_math) — + maxpool /
 upsample / KFPN kernels) and the fused sigmoid + decode (K=50), each
 captured as a HIP graph; with N > 1 the step also all-gathers the (16, 50, 10)
 detections over RCCL (frames are sharded: rank r owns its own 16 frames).
@@ -42,6 +42,16 @@ PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32, de
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
 # bf16x6 computes each f32 MAC as 6 bf16 MFMA products: its f32-equivalent ceiling
 PEAK_BF16X6_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
+# fp16x3: 3 fp16 MFMA products per f32 MAC (fp16 MFMA has the bf16 rate)
+PEAK_FP16X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 3
+MATHS = {"fp16x3": _lib.MATH_FP16X3, "bf16x6": _lib.MATH_BF16X6, "f32": _lib.MATH_F32}
+PEAKS = {"fp16x3": (PEAK_FP16X3_TFLOPS, "dense fp16 MFMA 2500 TF / 3 fp16 products per f32 MAC"),
+         "bf16x6": (PEAK_BF16X6_TFLOPS, "dense bf16 MFMA 2500 TF / 6 bf16 products per f32 MAC"),
+         "f32": (PEAK_FP32_MFMA_TFLOPS, "dense f32 MFMA (v_mfma_f32_32x32x2_f32)")}
+DTYPES = {"fp16x3": "f32 (fp16x3: power-of-two-scaled operands split into 2 fp16 terms, "
+                    "3 products, f32 accumulate)",
+          "bf16x6": "f32 (bf16x6: operands split into 3 bf16 terms, 6 products, f32 accumulate)",
+          "f32": "f32"}
 METRIC = "BEV frames/sec (608x608, bs=16)"
 
 
@@ -58,9 +68,10 @@ def parse():
                          "stream: KITTI .bin files read + DMA'd per batch (SURVEY §8(f) #3); "
                          "fusion: BASELINE configs[4] chain up to camera-LiDAR fusion + NMS "
                          "(use --batch 8)")
-    ap.add_argument("--math", choices=["bf16x6", "f32"],
-                    default="f32" if _lib.math_from_env() == _lib.MATH_F32 else "bf16x6",
-                    help="convolution arithmetic (include/sfa_hip.h sfa_math; default bf16x6)")
+    env_math = {v: k for k, v in MATHS.items()}[_lib.math_from_env()]
+    ap.add_argument("--math", choices=list(MATHS), default=env_math,
+                    help="convolution arithmetic (include/sfa_hip.h sfa_math; default: SFA_MATH "
+                         "or the library default)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--inflight", type=int, default=2,
                     help="steps in flight on separate streams (each with its own buffers and "
@@ -95,7 +106,7 @@ def build_pipeline(dev, args, rank):
     spec = _lib.state_layout(arch)
     sd = synthetic.synthetic_state_dict(spec, seed=0)
     engine = KfpnEngine(arch, pack_state_dict(sd, arch), dev,
-                        math=_lib.MATH_F32 if args.math == "f32" else _lib.MATH_BF16X6)
+                        math=MATHS[args.math])
     if args.workload == "e2e":
         clouds = [synthetic.synthetic_point_cloud(1000 * rank + i + 1) for i in range(args.batch)]
         pipe = DetectorPipeline(engine, args.batch, K=args.K, with_bev=True,
@@ -207,7 +218,7 @@ def run_stream(args, rank, world, dev):
     arch = _lib.make_arch(DEFAULT_HEADS)
     sd = synthetic.synthetic_state_dict(_lib.state_layout(arch), seed=0)
     engine = KfpnEngine(arch, pack_state_dict(sd, arch), dev,
-                        math=_lib.MATH_F32 if args.math == "f32" else _lib.MATH_BF16X6)
+                        math=MATHS[args.math])
     tmp = tempfile.mkdtemp(prefix=f"sfa_bins_r{rank}_", dir="/tmp")
     try:
         files = []
@@ -249,7 +260,7 @@ def run_fusion(args, rank, world, dev):
     arch = _lib.make_arch(DEFAULT_HEADS)
     sd = synthetic.synthetic_state_dict(_lib.state_layout(arch), seed=0)
     engine = KfpnEngine(arch, pack_state_dict(sd, arch), dev,
-                        math=_lib.MATH_F32 if args.math == "f32" else _lib.MATH_BF16X6)
+                        math=MATHS[args.math])
     cal = project_cases.calibs()["avg"]
     calib = runtime_make_calib(cal)
     clouds = [synthetic.synthetic_point_cloud(1000 * rank + i + 1) for i in range(args.batch)]
@@ -321,7 +332,7 @@ def main():
                 "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                 "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
                 "scaling": "weak", "vs_baseline": None,
-                "dtype": "f32 (bf16x6)" if args.math == "bf16x6" else "f32",
+                "dtype": DTYPES[args.math],
                 "data": data, "config": cfg,
             }), flush=True)
         if world > 1:
@@ -401,8 +412,7 @@ def main():
         flop_step = CONV_FLOP_PER_FRAME * args.batch
         # the forward's own event time with one step in flight (the conv launches + aux)
         achieved = flop_step / (fwd_ms * 1e-3) / 1e12
-        x6 = args.math == "bf16x6"
-        peak = PEAK_BF16X6_TFLOPS if x6 else PEAK_FP32_MFMA_TFLOPS
+        peak, peak_basis = PEAKS[args.math]
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -414,8 +424,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32 (bf16x6: operands split into 3 bf16 terms, 6 products, f32 accumulate)"
-                     if x6 else "f32",
+            "dtype": DTYPES[args.math],
             "data": "synthetic (hash-RNG U[0,1) BEV frames; synthetic He-uniform weights, BN folded)"
                     if args.workload == "bev_infer" else
                     "synthetic (132,880-pt LiDAR sweeps per frame, SURVEY §8(d); synthetic weights)",
@@ -435,13 +444,13 @@ def main():
                           "note": "one step in flight; value/ms_per_step use %d in flight" % nf},
             "roofline": {
                 "bound": "mfma",
-                "kernel": ("conv_x6_kernel / conv_x6g_kernel" if x6 else "conv_mfma_kernel") +
+                "kernel": ("conv_mfma_kernel" if args.math == "f32" else
+                           "conv_x6_kernel / conv_x6g_kernel (math %s)" % args.math) +
                           " (23 implicit-GEMM launches per forward; achieved = algorithmic f32 FLOP "
                           "over the whole forward's event time, aux kernels included)",
                 "achieved": round(achieved, 3),
                 "peak": round(peak, 2),
-                "peak_basis": ("dense bf16 MFMA 2500 TF / 6 bf16 products per f32 MAC" if x6 else
-                               "dense f32 MFMA (v_mfma_f32_32x32x2_f32)"),
+                "peak_basis": peak_basis,
                 "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4),
                 "frac_of_f32_mfma_peak": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),

@@ -105,7 +105,8 @@ int sfa_state_entry(const sfa_arch* arch, int index, char* name, int name_len, i
  * state_dict entry except *.num_batches_tracked, concatenated in
  * sfa_state_entry order.  BatchNorm (eps 1e-5) is folded into the preceding
  * convolution; conv weights are re-laid out OHWI / K-concatenated for the
- * implicit-GEMM kernels, each also stored as three bf16 terms for SFA_MATH_BF16X6.
+ * implicit-GEMM kernels, each also stored as three bf16 terms for SFA_MATH_BF16X6 and,
+ * scaled per output channel by a power of two, as two fp16 terms for SFA_MATH_FP16X3.
  * `packed` must hold sfa_packed_floats(arch) floats. */
 size_t sfa_state_floats(const sfa_arch* arch);
 size_t sfa_packed_floats(const sfa_arch* arch);
@@ -122,13 +123,18 @@ typedef struct sfa_model sfa_model;
 int sfa_model_create(const sfa_arch* arch, const float* packed_device, sfa_model** out);
 void sfa_model_destroy(sfa_model* model);
 
-/* Arithmetic of the convolutions (all results are f32; both modes meet the parity
+/* Arithmetic of the convolutions (all results are f32; every mode meets the parity
  * bar):
- *   SFA_MATH_BF16X6 (default) — every f32 operand split into three bf16 terms, the six
- *     significant products on bf16 MFMA with f32 accumulation: f32-level accuracy at
- *     ~2.7x the f32-MFMA rate (max rel. logit error vs the reference ~3e-6);
+ *   SFA_MATH_FP16X3 (default) — operands scaled by powers of two (weights per output channel at
+ *     pack time, activations per tensor and frame from the max |x| their producer records) and
+ *     split into two fp16 terms (22 significand bits), the three significant products on
+ *     fp16 MFMA with f32 accumulation: half the MFMA work of BF16X6 at the same accuracy
+ *     class (max rel. logit error vs the reference ~3e-6); the scales never overflow fp16
+ *     (scaled |x| < 2^14), and each frame is scaled by its own maxima (batch-invariant);
+ *   SFA_MATH_BF16X6 — every f32 operand split into three bf16 terms, the six significant
+ *     products on bf16 MFMA with f32 accumulation (full f32 exponent range, no scaling);
  *   SFA_MATH_F32 — v_mfma_f32_32x32x2_f32 (exact f32 FMA chains). */
-enum sfa_math { SFA_MATH_F32 = 0, SFA_MATH_BF16X6 = 1 };
+enum sfa_math { SFA_MATH_F32 = 0, SFA_MATH_BF16X6 = 1, SFA_MATH_FP16X3 = 2 };
 int sfa_model_set_math(sfa_model* model, int math);
 int sfa_model_get_math(const sfa_model* model);
 

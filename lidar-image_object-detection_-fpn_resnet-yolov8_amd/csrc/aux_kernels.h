@@ -12,7 +12,10 @@ struct KfpnOut {
   int total_ch;
 };
 
-int launch_nchw3_to_nhwc4(const float* x, float* y, int B, int H, int W, bool flip, hipStream_t st);
+// amax (nullable): per-frame max |y| words (conv.h, fp16x3 input scale)
+int launch_nchw3_to_nhwc4(const float* x, float* y, int B, int H, int W, bool flip, unsigned* amax,
+                          hipStream_t st);
+int launch_amax_nhwc4(const float* x, int B, int H, int W, unsigned* amax, hipStream_t st);
 int launch_maxpool3s2(const float* x, float* y, int B, int H, int W, int C, hipStream_t st);
 int launch_upsample2x(const float* x, float* y, int B, int H, int W, int C, hipStream_t st);
 int launch_kfpn(const float* L0, const float* L1, const float* L2, const KfpnOut& o, int B, int h,

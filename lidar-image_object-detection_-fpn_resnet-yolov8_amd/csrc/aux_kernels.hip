@@ -7,18 +7,41 @@
 //   sigmoid_clamp       utils/torch_utils.py:44-45
 #include "aux_kernels.h"
 
+#include <algorithm>
+
+#include "conv.h"
+
 namespace sfa {
 
 // FLIP: torch.flip(x, [H, W]) fused in (utils/demo_utils.py:110-111, the back view):
 // pixel (h, w) of the output reads (H-1-h, W-1-w), i.e. flat index HW-1-p.
 template <bool FLIP>
 __global__ void __launch_bounds__(256) nchw3_to_nhwc4_kernel(const float* __restrict__ x,
-                                                             float4* __restrict__ y, int B, int HW) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long long)B * HW) return;
-  const int b = (int)(i / HW), p = (int)(i - (long long)b * HW);
-  const float* s = x + (size_t)b * 3 * HW + (FLIP ? HW - 1 - p : p);
-  y[i] = make_float4(s[0], s[HW], s[2 * HW], 0.f);
+                                                             float4* __restrict__ y, int HW,
+                                                             unsigned* __restrict__ amax) {
+  __shared__ float red[8];
+  const int b = blockIdx.y;  // frame
+  float mx = 0.f;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
+    const float* s = x + (size_t)b * 3 * HW + (FLIP ? HW - 1 - p : p);
+    const float4 v = make_float4(s[0], s[HW], s[2 * HW], 0.f);
+    y[(size_t)b * HW + p] = v;
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fabsf(v.z)));
+  }
+  if (amax) amax_commit_block<4>(amax, b, mx, 0.f, red);  // fp16x3 input scale (conv.h)
+}
+
+// Per-frame max |x| of an NHWC4 input handed to the forward as is (fp16x3 input scale).
+__global__ void __launch_bounds__(256) amax_nhwc4_kernel(const float4* __restrict__ x, int HW,
+                                                         unsigned* __restrict__ amax) {
+  __shared__ float red[8];
+  const int b = blockIdx.y;
+  float mx = 0.f;
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < HW; p += gridDim.x * blockDim.x) {
+    const float4 v = x[(size_t)b * HW + p];
+    mx = fmaxf(mx, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  amax_commit_block<4>(amax, b, mx, 0.f, red);
 }
 
 // One thread per (output pixel, 4 channels).
@@ -139,14 +162,34 @@ __global__ void __launch_bounds__(256) sigmoid_clamp_kernel(float* __restrict__ 
 
 static unsigned grid_of(long long n) { return (unsigned)((n + 255) / 256); }
 
-int launch_nchw3_to_nhwc4(const float* x, float* y, int B, int H, int W, bool flip, hipStream_t st) {
-  const long long n = (long long)B * H * W;
+// grid: (blocks per frame, frames); grid-stride within a frame keeps the amax commits few
+static dim3 frame_grid(int B, long long HW) {
+  return dim3((unsigned)std::min<long long>((HW + 255) / 256, 128), (unsigned)B);
+}
+
+int launch_nchw3_to_nhwc4(const float* x, float* y, int B, int H, int W, bool flip, unsigned* amax,
+                          hipStream_t st) {
+  if (B > 65535) {
+    set_error("nchw3_to_nhwc4: batch %d too large", B);
+    return SFA_E_INVALID;
+  }
   if (flip)
-    hipLaunchKernelGGL(nchw3_to_nhwc4_kernel<true>, dim3(grid_of(n)), dim3(256), 0, st, x,
-                       reinterpret_cast<float4*>(y), B, H * W);
+    hipLaunchKernelGGL(nchw3_to_nhwc4_kernel<true>, frame_grid(B, (long long)H * W), dim3(256), 0, st,
+                       x, reinterpret_cast<float4*>(y), H * W, amax);
   else
-    hipLaunchKernelGGL(nchw3_to_nhwc4_kernel<false>, dim3(grid_of(n)), dim3(256), 0, st, x,
-                       reinterpret_cast<float4*>(y), B, H * W);
+    hipLaunchKernelGGL(nchw3_to_nhwc4_kernel<false>, frame_grid(B, (long long)H * W), dim3(256), 0,
+                       st, x, reinterpret_cast<float4*>(y), H * W, amax);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+int launch_amax_nhwc4(const float* x, int B, int H, int W, unsigned* amax, hipStream_t st) {
+  if (B > 65535) {
+    set_error("amax: batch %d too large", B);
+    return SFA_E_INVALID;
+  }
+  hipLaunchKernelGGL(amax_nhwc4_kernel, frame_grid(B, (long long)H * W), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(x), H * W, amax);
   SFA_LAUNCH_CHECK();
   return SFA_OK;
 }

@@ -47,6 +47,88 @@ inline bool make_seg(ConvSeg& g, const float* x, int B, int H, int W, int C, int
 
 enum ConvEpilogue { EPI_STD = 0, EPI_HEAD = 1 };
 
+// fp16x3 activation scales (SFA_MATH_FP16X3).  max |x| of an activation tensor is kept
+// PER FRAME (so a frame's result never depends on the rest of its batch), each in
+// SFA_AMAX_WORDS words: SFA_AMAX_SHARDS shards one 128-B line apart, shard = blockIdx & 7
+// of the producing workgroup; a reader takes the max over the shards.  Tensor t, frame b
+// lives at base_t + b * SFA_AMAX_WORDS.
+constexpr int SFA_AMAX_SHARDS = 8;
+constexpr int SFA_AMAX_STRIDE = 32;   // words between shards
+constexpr int SFA_AMAX_WORDS = SFA_AMAX_SHARDS * SFA_AMAX_STRIDE;
+
+__device__ __forceinline__ void amax_atomic(unsigned* amax, int frame, float v) {
+  atomicMax(amax + (size_t)frame * SFA_AMAX_WORDS + (blockIdx.x & (SFA_AMAX_SHARDS - 1)) * SFA_AMAX_STRIDE,
+            __float_as_uint(v));
+}
+
+// Block-wide commit of the maxima of frames fb0 (mx0) and fb0 + 1 (mx1): every thread of
+// the block calls it; one no-return atomic per frame and block.  `red` is 2 * NW floats of
+// LDS no wave is using (the call synchronises the block).
+template <int NW>
+__device__ __forceinline__ void amax_commit_block(unsigned* amax, int fb0, float mx0, float mx1,
+                                                  float* red) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    mx0 = fmaxf(mx0, __shfl_xor(mx0, o, 64));
+    mx1 = fmaxf(mx1, __shfl_xor(mx1, o, 64));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    red[2 * (threadIdx.x >> 6)] = mx0;
+    red[2 * (threadIdx.x >> 6) + 1] = mx1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m0 = red[0], m1 = red[1];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      m0 = fmaxf(m0, red[2 * w]);
+      m1 = fmaxf(m1, red[2 * w + 1]);
+    }
+    if (m0 > 0.f) amax_atomic(amax, fb0, m0);
+    if (m1 > 0.f) amax_atomic(amax, fb0 + 1, m1);  // only rows of a real frame raise it
+  }
+}
+
+// Scale of frame `frame` for an fp16x3 consumer: 2^(13 - e) for max |x| in [2^e, 2^(e+1))
+// over its segments' inputs, so every scaled |x| < 2^14 (4x below the fp16 maximum);
+// zero / unset / non-finite max -> 1.  sinv = 1 / s.
+__device__ __forceinline__ float amax_frame_scale(const unsigned* const (&amax)[2], int nseg,
+                                                  int frame, float& sinv) {
+  unsigned mb = 0;
+  for (int sg = 0; sg < nseg; ++sg)
+    if (amax[sg]) {
+      const unsigned* p = amax[sg] + (size_t)frame * SFA_AMAX_WORDS;
+#pragma unroll
+      for (int j = 0; j < SFA_AMAX_SHARDS; ++j) mb = max(mb, p[j * SFA_AMAX_STRIDE]);
+    }
+  if (mb == 0 || mb >= 0x7f800000u) {
+    sinv = 1.f;
+    return 1.f;
+  }
+  int e = (int)(mb >> 23) - 127;
+  e = e < -100 ? -100 : (e > 100 ? 100 : e);
+  sinv = __uint_as_float((unsigned)(127 - 13 + e) << 23);
+  return __uint_as_float((unsigned)(127 + 13 - e) << 23);
+}
+
+// Producer side of a conv epilogue (rows m of the output, P = OH * OW rows per frame):
+// frames fb0 and fb0 + 1 are reduced over the block, rows of later frames (blocks taller
+// than a frame: small maps) are committed one by one.
+struct AmaxRows {
+  int P, fb0, mb1, mb2;
+  float mx0 = 0.f, mx1 = 0.f;
+  __device__ AmaxRows(int P_, int m0) : P(P_), fb0(m0 / P_), mb1((m0 / P_ + 1) * P_), mb2(mb1 + P_) {}
+  __device__ __forceinline__ void add(unsigned* amax, int m, float val) {
+    const float v = fabsf(val);
+    if (m < mb1)
+      mx0 = fmaxf(mx0, v);
+    else if (m < mb2)
+      mx1 = fmaxf(mx1, v);
+    else if (v > 0.f)
+      amax_atomic(amax, m / P, v);
+  }
+};
+
 struct ConvArgs {
   ConvSeg seg[2];
   int nseg;
@@ -54,6 +136,13 @@ struct ConvArgs {
   int Kpad;            // total K (multiple of 16)
   const float* w;      // [N][Kpad] (OHWI per segment, K-concatenated, zero padded)
   const uint16_t* wx;  // bf16x6 path: w split into 3 bf16 terms, [3][N][Kpad]
+  // fp16x3 path: w[n][k] * 2^e[n] split into 2 fp16 terms, [2][N][Kpad]; winv[n] = 2^-e[n]
+  const uint16_t* wh;
+  const float* winv;
+  // fp16x3 path: per K-segment, the per-frame max |x| words of that segment's input
+  // (written by its producer; frame b at + b * SFA_AMAX_WORDS), or null (scale 1)
+  const unsigned* amax_in[2];
+  unsigned* amax_out;  // this conv's per-frame max |y| is recorded here, or null
   const float* bias;   // [N]
   const float* res;    // residual [M][N] (NHWC) or nullptr
   float* y;            // output [M][N] (NHWC)

@@ -28,6 +28,35 @@ static int launch_conv_x6(const ConvArgs& a, int epilogue, hipStream_t st) {
   return rc;
 }
 
+// fp16x3 tiles per shape (tools/convbench.hip, profiles/r01_convbench_h3.txt): BK = 32
+// with a 2-deep ring where K allows it (half the barriers per MAC), 256-row tiles for
+// the 64-wide and the big-M layers.  Returns SFA_E_UNSUPPORTED when no tile fits.
+static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
+  if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;
+  auto ok = [](int rc) { return rc != SFA_E_UNSUPPORTED; };
+  int rc = SFA_E_UNSUPPORTED;
+  if (epilogue == EPI_HEAD) {
+    if (a.N == 320) {
+      rc = launch_conv_x6g_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, 0, 320, 1>(a, st);
+      if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 320, 32, EPI_HEAD, 1, 16, 3, 0, 320, 1>(a, st);
+    }
+    if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_HEAD, 1, 16, 3, 0, 64, 1>(a, st);
+    return rc;
+  }
+  if (a.N == 64) {
+    if (a.M >= 50000) rc = launch_conv_x6g_cfg<128, 64, 32, EPI_STD, 2, 32, 2, 0, 64, 1>(a, st);
+    if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_STD, 1, 16, 3, 0, 64, 1>(a, st);
+    return rc;
+  }
+  if (a.N % 128 == 0) {
+    if (a.M >= 50000) rc = launch_conv_x6g_cfg<256, 128, 32, EPI_STD, 1, 16, 3, 0, 128, 1>(a, st);
+    else if (a.M >= 10000) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2, 32, 2, 0, 128, 1>(a, st);
+    else rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 1, 32, 3, 0, 128, 1>(a, st);
+    if (!ok(rc)) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2, 16, 3, 0, 128, 1>(a, st);
+  }
+  return rc;
+}
+
 int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t st) {
   // Host-side shape checks: the kernels assume these and never bounds-check them.
   if (a.N <= 0 || a.N % 64 != 0 || a.M <= 0 || a.Kpad <= 0 || a.Kpad % 16 != 0) {
@@ -53,7 +82,11 @@ int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t st) {
     set_error("conv: bad kseg1 %d", a.kseg1);
     return SFA_E_UNSUPPORTED;
   }
-  if (math == SFA_MATH_BF16X6) {
+  if (math == SFA_MATH_FP16X3) {
+    const int rc = launch_conv_h3(a, epilogue, st);
+    if (rc != SFA_E_UNSUPPORTED) return rc;
+  }
+  if (math == SFA_MATH_BF16X6 || math == SFA_MATH_FP16X3) {
     const int rc = launch_conv_x6(a, epilogue, st);
     if (rc != SFA_E_UNSUPPORTED) return rc;
   }

@@ -230,6 +230,7 @@ __global__ void __launch_bounds__(256, OCC) conv_mfma_kernel(const ConvArgs a) {
   }
 
   if constexpr (EPI == EPI_STD) {
+    AmaxRows am(a.OH * a.OW, m0);
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
       const int n = n0 + wn * WN + ni * 32 + r;
@@ -244,10 +245,14 @@ __global__ void __launch_bounds__(256, OCC) conv_mfma_kernel(const ConvArgs a) {
             if (a.res) val += a.res[(size_t)m * a.N + n];
             if (a.relu) val = fmaxf(val, 0.f);
             a.y[(size_t)m * a.N + n] = val;
+            if (a.amax_out) am.add(a.amax_out, m, val);
           }
         }
       }
     }
+    // consumers on the fp16x3 path scale by this (conv.h); the K loop's last barrier
+    // retired every LDS read
+    if (a.amax_out) amax_commit_block<4>(a.amax_out, am.fb0, am.mx0, am.mx1, smem);
   } else {
     // Detection head: ReLU(conv3x3 + b) staged in LDS (HCH rows at a time), then
     // the head's 1x1 conv (64 -> c <= 4) with bias, written channel-planar.

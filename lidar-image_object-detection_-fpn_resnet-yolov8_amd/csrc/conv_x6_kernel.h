@@ -33,6 +33,8 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float x6_f32x16 __attribute__((ext_vector_type(16)));
 typedef float x6_f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned x6_u32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8_t __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void split3(const x6_f32x4 v, bf16x4_t& t0, bf16x4_t& t1, bf16x4_t& t2) {
 #pragma unroll
@@ -46,33 +48,60 @@ __device__ __forceinline__ void split3(const x6_f32x4 v, bf16x4_t& t0, bf16x4_t&
   }
 }
 
+// fp16x3: x * s = hi + lo with hi = fp16(x * s), lo = fp16(x * s - hi) (the difference is
+// exact in f32): 22 significand bits; s is a power of two, so x * s is exact.
+__device__ __forceinline__ void split2h(const x6_f32x4 v, float s, f16x4_t& t0, f16x4_t& t1) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float x = v[i] * s;
+    const _Float16 hi = (_Float16)x;
+    t0[i] = hi;
+    t1[i] = (_Float16)(x - (float)hi);
+  }
+}
+
 // Shared epilogue of the bf16x6 kernels (the accumulator layout of every 32x32 MFMA:
 // lane (r, h), register v -> row (v & 3) + 8 (v >> 2) + 4h, column r).
-template <int BM, int BN, int WM, int WN, int TM, int TN, int NT, int EPI>
+// PREC 1 (fp16x3): the accumulator of row R holds sum (x s_R)(w 2^e[n]); it is scaled
+// back by 1/s_R (ainv[mi] of the lane holding row R as its A row) and winv[n], both
+// powers of two, before the bias.  amax_out: the output's per-frame max |y| (conv.h).
+template <int BM, int BN, int WM, int WN, int TM, int TN, int NT, int EPI, int PREC = 0>
 __device__ __forceinline__ void x6_epilogue(const ConvArgs& a, x6_f32x16 (&acc)[TM][TN],
                                             unsigned char* smem, int m0, int n0, int nt, int wm,
-                                            int wn, int tid) {
+                                            int wn, int tid, const float (&ainv)[TM]) {
   constexpr int HCH = BM < 128 ? BM : 128;
   const int M = a.M, lane = tid & 63, r = lane & 31, h = lane >> 5;
+  // row scales in accumulator order (lane (r, h), register v -> tile row (v&3)+8(v>>2)+4h)
+  float rinv[TM][16];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+    for (int v = 0; v < 16; ++v)
+      rinv[mi][v] = PREC ? __shfl(ainv[mi], (v & 3) + 8 * (v >> 2) + 4 * h, 64) : 1.f;
   if constexpr (EPI == EPI_STD) {
+    AmaxRows am(a.OH * a.OW, m0);
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
       const int n = n0 + wn * WN + ni * 32 + r;
       const float bn = a.bias[n];
+      const float cs = PREC ? a.winv[n] : 1.f;
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
           const int m = m0 + wm * WM + mi * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
           if (m < M) {
-            float val = acc[mi][ni][v] + bn;
+            float val = (PREC ? acc[mi][ni][v] * rinv[mi][v] * cs : acc[mi][ni][v]) + bn;
             if (a.res) val += a.res[(size_t)m * a.N + n];
             if (a.relu) val = fmaxf(val, 0.f);
             a.y[(size_t)m * a.N + n] = val;
+            if (a.amax_out) am.add(a.amax_out, m, val);
           }
         }
       }
     }
+    if (a.amax_out)
+      amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1, reinterpret_cast<float*>(smem));
   } else {
     // BN = 64 * HPB: heads nt*HPB .. nt*HPB + HPB - 1 (head_conv = 64 channels each);
     // per head: ReLU(conv3x3 + b) staged in LDS, then its 1x1 conv, channel-planar out
@@ -96,12 +125,14 @@ __device__ __forceinline__ void x6_epilogue(const ConvArgs& a, x6_f32x16 (&acc)[
           const int col = wn * WN + ni * 32 + r - 64 * hh;  // column within the head
           if (col < 0 || col >= 64) continue;
           const float bn = a.bias[n0 + 64 * hh + col];
+          const float cs = PREC ? a.winv[n0 + 64 * hh + col] : 1.f;
 #pragma unroll
           for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
             for (int v = 0; v < 16; ++v) {
               const int row = wm * WM + mi * 32 + (v & 3) + 8 * (v >> 2) + 4 * h - c0;
-              if (row >= 0 && row < HCH) T[row * 65 + col] = fmaxf(acc[mi][ni][v] + bn, 0.f);
+              if (row >= 0 && row < HCH)
+                T[row * 65 + col] = fmaxf((PREC ? acc[mi][ni][v] * rinv[mi][v] * cs : acc[mi][ni][v]) + bn, 0.f);
             }
         }
         __syncthreads();
@@ -307,7 +338,8 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_x6_kerne
     __syncthreads();
   }
 
-  x6_epilogue<BM, BN, WM, WN, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wm, wn, tid);
+  const float one[TM] = {};
+  x6_epilogue<BM, BN, WM, WN, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wm, wn, tid, one);
 }
 
 // LDS-DMA variant: A (f32) and the three W terms (bf16) stream into an NSTAGE-deep
@@ -322,8 +354,10 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_x6_kerne
 // ABL: diagnostic ablation bits for tools/convbench (0 in the product): 1 = no DMA in
 // the K loop, 2 = no A split (raw bits as terms), 4 = W fragments read once per k-step
 // group instead of per column block, 8 = no barrier.
+// PREC 1: the fp16x3 form (two fp16 W terms, scaled A split into two fp16 terms when read,
+// products hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_f16).
 template <int BM, int BN, int WM, int EPI, int OCC, int BK = 16, int NSTAGE = 3, int ABL = 0,
-          int WNT = BN>
+          int WNT = BN, int PREC = 0>
 __global__ void __launch_bounds__((BM / WM) * (BN / WNT) * 64, OCC) conv_x6g_kernel(const ConvArgs a) {
   static_assert(BK == 16 || BK == 32, "BK");
   static_assert(NSTAGE == 2 || NSTAGE == 3, "ring depth");
@@ -334,12 +368,13 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WNT) * 64, OCC) conv_x6g_ker
   constexpr int TM = WM / 32, TN = WN / 32;
   constexpr int KST = BK / 16;
   constexpr int AROW = BK * 4, BROW = BK * 2;         // bytes per LDS row
+  constexpr int NTW = PREC ? 2 : 3;                   // W terms
   constexpr int A_BYTES = BM * AROW, TERM_B = BN * BROW;
-  constexpr int STAGE = A_BYTES + 3 * TERM_B;
+  constexpr int STAGE = A_BYTES + NTW * TERM_B;
   constexpr int A_RPD = 1024 / AROW, B_RPD = 1024 / BROW;  // rows per DMA instruction
   constexpr int ND_A = BM / A_RPD;
   constexpr int ND_BT = BN / B_RPD;                         // per term
-  constexpr int ND = ND_A + 3 * ND_BT;
+  constexpr int ND = ND_A + NTW * ND_BT;
   constexpr int DPW = (ND + NW - 1) / NW;  // max per wave
   constexpr int DREM = ND % NW;            // waves < DREM issue DPW, the rest DPW - 1 (if DREM)
   static_assert(BM % A_RPD == 0 && BN % B_RPD == 0 && BN % 32 == 0, "tile");
@@ -397,7 +432,17 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WNT) * 64, OCC) conv_x6g_ker
       (int)(a.nseg > 1 ? a.seg[1].bytes : a.seg[0].bytes), 0x00020000);
   const unsigned term_bytes = (unsigned)a.N * (unsigned)a.Kpad * 2u;
   const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(a.wx), (short)0, (int)(3u * term_bytes), 0x00020000);
+      const_cast<uint16_t*>(PREC ? a.wh : a.wx), (short)0, (int)(NTW * term_bytes), 0x00020000);
+  // fp16x3: per A row (this lane's row of each 32-row MFMA tile) the scale of its frame
+  float as[TM], ainv[TM];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+    as[mi] = ainv[mi] = 1.f;
+    if constexpr (PREC == 1) {
+      const int m = min(m0 + wm * WM + mi * 32 + (lane & 31), M - 1);
+      as[mi] = amax_frame_scale(a.amax_in, a.nseg, m / (a.OH * a.OW), ainv[mi]);
+    }
+  }
   // W lanes: row brow_in of the instruction's B_RPD rows, chunk (lane % CPR)
   constexpr int CPR = BROW / 16;
   const int brow_in = lane / CPR;
@@ -460,6 +505,37 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WNT) * 64, OCC) conv_x6g_ker
     const unsigned char* SB = S + A_BYTES;
 #pragma unroll
     for (int s = 0; s < KST; ++s) {
+      if constexpr (PREC == 1) {
+        f16x8_t hf[2][TM];
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) {
+          const int R = wm * WM + mi * 32 + r;
+          const int q = 4 * s + 2 * h;
+          const x6_f32x4 q0 = *reinterpret_cast<const x6_f32x4*>(S + R * AROW + ((q ^ swzA(R)) << 4));
+          const x6_f32x4 q1 = *reinterpret_cast<const x6_f32x4*>(S + R * AROW + (((q + 1) ^ swzA(R)) << 4));
+          f16x4_t t0, t1, u0, u1;
+          split2h(q0, as[mi], t0, t1);
+          split2h(q1, as[mi], u0, u1);
+          hf[0][mi] = __builtin_shufflevector(t0, u0, 0, 1, 2, 3, 4, 5, 6, 7);
+          hf[1][mi] = __builtin_shufflevector(t1, u1, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni) {
+          const int R = wn * WN + ni * 32 + r;
+          const int byte = R * BROW + (((2 * s + h) ^ swzB(R)) << 4);
+          const f16x8_t b0 = *reinterpret_cast<const f16x8_t*>(SB + byte);
+          const f16x8_t b1 = *reinterpret_cast<const f16x8_t*>(SB + TERM_B + byte);
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi) {
+            x6_f32x16 c = acc[mi][ni];
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(hf[1][mi], b0, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(hf[0][mi], b1, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(hf[0][mi], b0, c, 0, 0, 0);
+            acc[mi][ni] = c;
+          }
+        }
+        continue;
+      }
       bf16x8_t af[3][TM];
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
@@ -529,13 +605,13 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WNT) * 64, OCC) conv_x6g_ker
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  x6_epilogue<BM, BN, WM, WN, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wm, wn, tid);
+  x6_epilogue<BM, BN, WM, WN, TM, TN, NT, EPI, PREC>(a, acc, smem, m0, n0, nt, wm, wn, tid, ainv);
 }
 
 template <int BM, int BN, int WM, int EPI, int OCC, int BK = 16, int NSTAGE = 3, int ABL = 0,
-          int WNT = BN>
+          int WNT = BN, int PREC = 0>
 inline int launch_conv_x6g_cfg(const ConvArgs& a, hipStream_t st) {
-  if (!a.wx || a.Kpad % BK != 0 || (a.nseg == 2 && a.kseg1 % BK != 0) || a.N % BN != 0) {
+  if (!(PREC ? a.wh != nullptr && a.winv != nullptr : a.wx != nullptr) || a.Kpad % BK != 0 || (a.nseg == 2 && a.kseg1 % BK != 0) || a.N % BN != 0) {
     set_error("conv_x6g: K/N not aligned to the tile or no split weights (Kpad=%d kseg1=%d N=%d)",
               a.Kpad, a.kseg1, a.N);
     return SFA_E_UNSUPPORTED;
@@ -549,7 +625,7 @@ inline int launch_conv_x6g_cfg(const ConvArgs& a, hipStream_t st) {
     set_error("conv_x6g: bad grid (M=%d N=%d)", a.M, a.N);
     return SFA_E_INVALID;
   }
-  hipLaunchKernelGGL((conv_x6g_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, ABL, WNT>),
+  hipLaunchKernelGGL((conv_x6g_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, ABL, WNT, PREC>),
                      dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WNT) * 64), 0, st, a);
   SFA_LAUNCH_CHECK();
   return SFA_OK;

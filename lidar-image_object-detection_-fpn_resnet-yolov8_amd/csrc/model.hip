@@ -119,13 +119,14 @@ static std::vector<Entry> state_layout(const sfa_arch* a) {
 
 // ----------------------------------------------------------- packed layout
 // Offsets in floats into the packed buffer.  wx: the same weights split into three
-// bf16 terms [3][N][Kpad] for the bf16x6 kernels (conv_x6_kernel.h).
+// bf16 terms [3][N][Kpad] for the bf16x6 kernels (conv_x6_kernel.h); wh / winv: the
+// fp16x3 form, W[n][k] * 2^e[n] as two fp16 terms [2][N][Kpad] and winv[n] = 2^-e[n].
 struct PConv {
-  size_t w, b, wx;
+  size_t w, b, wx, wh, winv;
   int N, K, Kpad;
 };
 struct PHeads {
-  size_t w3, b3, w1, b1, wx;
+  size_t w3, b3, w1, b1, wx, wh, winv;
   int N, K;
 };
 struct Plan {
@@ -152,6 +153,8 @@ static Plan make_plan(const sfa_arch* a) {
     c.w = take((size_t)N * c.Kpad);
     c.b = take(N);
     c.wx = take(((size_t)3 * N * c.Kpad + 1) / 2);
+    c.wh = take((size_t)N * c.Kpad);
+    c.winv = take(N);
     return c;
   };
   p.stem = conv(64, 49 * 4);
@@ -178,6 +181,8 @@ static Plan make_plan(const sfa_arch* a) {
     h.w1 = take((size_t)a->num_heads * 4 * 64);
     h.b1 = take((size_t)a->num_heads * 4);
     h.wx = take(((size_t)3 * h.N * h.K + 1) / 2);
+    h.wh = take((size_t)h.N * h.K);
+    h.winv = take(h.N);
   }
   p.total = cur;
   return p;
@@ -236,6 +241,32 @@ static void split_terms(const float* w, size_t n, uint16_t* out) {
       float bf;
       memcpy(&bf, &u, 4);
       x -= bf;
+    }
+  }
+}
+
+// fp16x3 form of W [N][K]: per output channel n, e[n] = floor(log2 max_k |W[n][k]|) and
+// W * 2^(13 - e[n]) (every |.| < 2^14) = hi + lo with hi = fp16(.) and lo = fp16(. - hi);
+// winv[n] = 2^(e[n] - 13).  Zero rows keep scale 1.
+static void split_terms_h3(const float* w, int N, int K, uint16_t* out, float* winv) {
+  const size_t n = (size_t)N * K;
+  for (int o = 0; o < N; ++o) {
+    float mx = 0.f;
+    for (int k = 0; k < K; ++k) mx = std::max(mx, std::fabs(w[(size_t)o * K + k]));
+    int e = 13;
+    if (mx > 0.f) {
+      (void)std::frexp(mx, &e);  // mx in [2^(e-1), 2^e)
+      e -= 1;
+    }
+    const float sc = std::ldexp(1.f, 13 - e);
+    winv[o] = std::ldexp(1.f, e - 13);
+    for (int k = 0; k < K; ++k) {
+      const size_t i = (size_t)o * K + k;
+      const float x = w[i] * sc;
+      const _Float16 hi = (_Float16)x;
+      const _Float16 lo = (_Float16)(x - (float)hi);
+      memcpy(out + i, &hi, 2);
+      memcpy(out + n + i, &lo, 2);
     }
   }
 }
@@ -367,18 +398,23 @@ extern "C" int sfa_pack_weights(const sfa_arch* arch, const float* state, size_t
       }
     }
   }
-  // bf16x6 terms of every implicit-GEMM weight matrix
+  // bf16x6 and fp16x3 terms of every implicit-GEMM weight matrix
   auto split = [&](const PConv& c) {
     split_terms(packed + c.w, (size_t)c.N * c.Kpad, reinterpret_cast<uint16_t*>(packed + c.wx));
+    split_terms_h3(packed + c.w, c.N, c.Kpad, reinterpret_cast<uint16_t*>(packed + c.wh),
+                   packed + c.winv);
   };
   split(p.stem);
   for (int li = 0; li < 4; ++li)
     for (int bi = 0; bi < 2; ++bi)
       for (int ci = 0; ci < 2; ++ci) split(p.blk[li][bi][ci]);
   for (int i = 0; i < 3; ++i) split(p.fpn[i]);
-  for (int f = 0; f < 3; ++f)
-    split_terms(packed + p.heads[f].w3, (size_t)p.heads[f].N * p.heads[f].K,
-                reinterpret_cast<uint16_t*>(packed + p.heads[f].wx));
+  for (int f = 0; f < 3; ++f) {
+    const PHeads& hp = p.heads[f];
+    split_terms(packed + hp.w3, (size_t)hp.N * hp.K, reinterpret_cast<uint16_t*>(packed + hp.wx));
+    split_terms_h3(packed + hp.w3, hp.N, hp.K, reinterpret_cast<uint16_t*>(packed + hp.wh),
+                   packed + hp.winv);
+  }
   return SFA_OK;
 }
 
@@ -390,7 +426,7 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   m->arch = *arch;
   m->w = packed_device;
   m->plan = make_plan(arch);
-  m->math = SFA_MATH_BF16X6;
+  m->math = SFA_MATH_FP16X3;
   if (hipGetDevice(&m->device) != hipSuccess ||
       hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&m->fork, hipEventDisableTiming) != hipSuccess ||
@@ -413,7 +449,8 @@ extern "C" void sfa_model_destroy(sfa_model* model) {
 
 extern "C" int sfa_model_set_math(sfa_model* model, int math) {
   SFA_CHECK_ARG(model, "set_math: null model");
-  SFA_CHECK_ARG(math == SFA_MATH_F32 || math == SFA_MATH_BF16X6, "set_math: unknown mode %d", math);
+  SFA_CHECK_ARG(math == SFA_MATH_F32 || math == SFA_MATH_BF16X6 || math == SFA_MATH_FP16X3,
+                "set_math: unknown mode %d", math);
   model->math = math;
   return SFA_OK;
 }
@@ -424,8 +461,14 @@ namespace sfa {
 
 // Activation buffers of one forward (NHWC f32), carved from the workspace.
 struct Bufs {
-  size_t xin, s0, p0, t[4], a[4], l[4], up1, c1, up2, c2, up3, up4, L0, L1, L2, total;
+  size_t xin, s0, p0, t[4], a[4], l[4], up1, c1, up2, c2, up3, up4, L0, L1, L2, amax, total;
 };
+
+// fp16x3 activation maxima (conv.h): per tensor a conv reads (named by its producer), B
+// frames of SFA_AMAX_WORDS words.  Pooling and bilinear upsampling never raise max |x|, so their
+// outputs share their input's slot.
+enum AmaxSlot { AM_INPUT = 0, AM_STEM = 1, AM_BLK = 2 /* + 4 li + 2 bi + ci */, AM_FPN = 18,
+                AM_COUNT = 21 };
 
 static Bufs plan_bufs(const sfa_arch* arch, int B, int H, int W) {
   Bufs b;
@@ -458,6 +501,7 @@ static Bufs plan_bufs(const sfa_arch* arch, int B, int H, int W) {
   b.L0 = take((size_t)nch * B * P8);
   b.L1 = take((size_t)nch * B * P4);
   b.L2 = take((size_t)nch * B * P4);
+  b.amax = take((size_t)AM_COUNT * B * SFA_AMAX_WORDS);
   b.total = cur;
   return b;
 }
@@ -476,6 +520,8 @@ static ConvArgs conv_args(const float* wbase, const PConv& pc, int B, int OH, in
   a.Kpad = pc.Kpad;
   a.w = wbase + pc.w;
   a.wx = reinterpret_cast<const uint16_t*>(wbase + pc.wx);
+  a.wh = reinterpret_cast<const uint16_t*>(wbase + pc.wh);
+  a.winv = wbase + pc.winv;
   a.bias = wbase + pc.b;
   a.res = res;
   a.y = y;
@@ -541,21 +587,39 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   const float* wb = m->w;
   const Plan& p = m->plan;
 
+  // fp16x3: every conv input's max |x| is recorded by its producer (slots zeroed here)
+  const bool h3 = m->math == SFA_MATH_FP16X3;
+  auto AM = [&](int slot) -> unsigned* {
+    return h3 ? reinterpret_cast<unsigned*>(ws + bf.amax) + (size_t)slot * B * SFA_AMAX_WORDS : nullptr;
+  };
+  auto blk_slot = [](int li, int bi, int ci) { return AM_BLK + 4 * li + 2 * bi + ci; };
+  if (h3) SFA_HIP_TRY(hipMemsetAsync(ws + bf.amax, 0, (size_t)AM_COUNT * B * SFA_AMAX_WORDS * 4, st));
+  auto io = [&](ConvArgs& a, int in0, int in1, int out) {
+    a.amax_in[0] = in0 >= 0 ? AM(in0) : nullptr;
+    a.amax_in[1] = in1 >= 0 ? AM(in1) : nullptr;
+    a.amax_out = out >= 0 ? AM(out) : nullptr;
+  };
+
   const float* xin = x;
   if (in_layout != SFA_IN_NHWC4) {
-    SFA_RC(launch_nchw3_to_nhwc4(x, F(bf.xin), B, H, W, in_layout == SFA_IN_NCHW3_FLIP_HW, st));
+    SFA_RC(launch_nchw3_to_nhwc4(x, F(bf.xin), B, H, W, in_layout == SFA_IN_NCHW3_FLIP_HW,
+                                 AM(AM_INPUT), st));
     xin = F(bf.xin);
+  } else if (h3) {
+    SFA_RC(launch_amax_nhwc4(x, B, H, W, AM(AM_INPUT), st));
   }
   const int H2 = H / 2, W2 = W / 2;
   // stem conv7x7/s2/p3 + BN + ReLU   (fpn_resnet.py:179-181)
   {
     ConvArgs a = conv_args(wb, p.stem, B, H2, W2, F(bf.s0), nullptr, 1);
     a.seg[0] = seg(xin, B, H, W, 4, 7, 2, 3);
+    io(a, AM_INPUT, -1, AM_STEM);
     SFA_RC(launch_conv(a, EPI_STD, m->math, st));
   }
   SFA_RC(launch_maxpool3s2(F(bf.s0), F(bf.p0), B, H2, W2, 64, st));  // :182
   // residual layers (fpn_resnet.py:184-187)
   const float* xcur = F(bf.p0);
+  int xslot = AM_STEM;  // maxpool keeps the stem's max
   int h = H / 4, w = W / 4, cin = 64;
   for (int li = 0; li < 4; ++li) {
     const int planes = 64 << li;
@@ -568,6 +632,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     {
       ConvArgs a = conv_args(wb, p.blk[li][0][0], B, oh, ow, t, nullptr, 1);
       a.seg[0] = seg(xcur, B, h, w, cin, 3, stride, 1);
+      io(a, xslot, -1, blk_slot(li, 0, 0));
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     {
@@ -578,20 +643,24 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
         a.kseg1 = 9 * planes;
         a.seg[1] = seg(xcur, B, h, w, cin, 1, stride, 0);
       }
+      io(a, blk_slot(li, 0, 0), li > 0 ? xslot : -1, blk_slot(li, 0, 1));
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     // block 1
     {
       ConvArgs a = conv_args(wb, p.blk[li][1][0], B, oh, ow, t, nullptr, 1);
       a.seg[0] = seg(av, B, oh, ow, planes, 3, 1, 1);
+      io(a, blk_slot(li, 0, 1), -1, blk_slot(li, 1, 0));
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     {
       ConvArgs a = conv_args(wb, p.blk[li][1][1], B, oh, ow, lv, av, 1);
       a.seg[0] = seg(t, B, oh, ow, planes, 3, 1, 1);
+      io(a, blk_slot(li, 1, 0), -1, blk_slot(li, 1, 1));
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     xcur = lv;
+    xslot = blk_slot(li, 1, 1);
     h = oh;
     w = ow;
     cin = planes;
@@ -606,6 +675,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.kseg1 = 512;
     a.seg[0] = seg(F(bf.up1), B, H16, W16, 512, 1, 1, 0);
     a.seg[1] = seg(F(bf.l[2]), B, H16, W16, 256, 1, 1, 0);
+    io(a, blk_slot(3, 1, 1), blk_slot(2, 1, 1), AM_FPN + 0);  // up1 = upsample(layer4)
     SFA_RC(launch_conv(a, EPI_STD, m->math, st));
   }
   SFA_RC(launch_upsample2x(F(bf.c1), F(bf.up2), B, H16, W16, 256, st));
@@ -629,6 +699,9 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.Kpad = hp.K;
     a.w = wb + hp.w3;
     a.wx = reinterpret_cast<const uint16_t*>(wb + hp.wx);
+    a.wh = reinterpret_cast<const uint16_t*>(wb + hp.wh);
+    a.winv = wb + hp.winv;
+    a.amax_in[0] = AM(AM_FPN + f);  // up2 / up3 / up4 come from conv_up_level1/2/3
     a.bias = wb + hp.b3;
     a.M = B * lh[f] * lw[f];
     a.N = hp.N;
@@ -664,6 +737,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.kseg1 = 256;
     a.seg[0] = seg(F(bf.up2), B, H8, W8, 256, 1, 1, 0);
     a.seg[1] = seg(F(bf.l[1]), B, H8, W8, 128, 1, 1, 0);
+    io(a, AM_FPN + 0, blk_slot(1, 1, 1), AM_FPN + 1);
     SFA_RC(launch_conv(a, EPI_STD, m->math, st));
   }
   SFA_RC(launch_upsample2x(F(bf.c2), F(bf.up3), B, H8, W8, 128, st));
@@ -673,6 +747,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.kseg1 = 128;
     a.seg[0] = seg(F(bf.up3), B, H4, W4, 128, 1, 1, 0);
     a.seg[1] = seg(F(bf.l[0]), B, H4, W4, 64, 1, 1, 0);
+    io(a, AM_FPN + 1, blk_slot(0, 1, 1), AM_FPN + 2);
     SFA_RC(launch_conv(a, EPI_STD, m->math, st));
   }
   SFA_RC(launch_head(1, st));

@@ -72,13 +72,13 @@ _PROTOS = {
                             _vp, _vp, _c_size, _vp]),
 }
 
-MATH_F32, MATH_BF16X6 = 0, 1
+MATH_F32, MATH_BF16X6, MATH_FP16X3 = 0, 1, 2
 _PROTOS["sfa_model_set_math"] = (_c_int, [_vp, _c_int])
 _PROTOS["sfa_model_get_math"] = (_c_int, [_vp])
 
 
-def math_from_env(default=MATH_BF16X6) -> int:
-    """SFA_MATH=f32 | bf16x6 selects the convolution arithmetic (include/sfa_hip.h)."""
+def math_from_env(default=MATH_FP16X3) -> int:
+    """SFA_MATH=f32 | bf16x6 | fp16x3 selects the convolution arithmetic (include/sfa_hip.h)."""
     v = os.environ.get("SFA_MATH", "").strip().lower()
     if not v:
         return default
@@ -86,7 +86,9 @@ def math_from_env(default=MATH_BF16X6) -> int:
         return MATH_F32
     if v in ("bf16x6", "x6"):
         return MATH_BF16X6
-    raise ValueError(f"SFA_MATH={v!r}: expected 'f32' or 'bf16x6'")
+    if v in ("fp16x3", "h3"):
+        return MATH_FP16X3
+    raise ValueError(f"SFA_MATH={v!r}: expected 'f32', 'bf16x6' or 'fp16x3'")
 
 
 class SfaFusionParams(ctypes.Structure):

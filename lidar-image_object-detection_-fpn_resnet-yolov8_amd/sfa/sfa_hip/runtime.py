@@ -79,7 +79,7 @@ class KfpnEngine:
         self.set_math(_lib.math_from_env() if math is None else math)
 
     def set_math(self, math: int):
-        """_lib.MATH_BF16X6 (default) or _lib.MATH_F32 for every convolution."""
+        """_lib.MATH_FP16X3 (default), _lib.MATH_BF16X6 or _lib.MATH_F32 for every convolution."""
         check(lib().sfa_model_set_math(self._h, int(math)), "sfa_model_set_math")
         self.math = int(math)
 

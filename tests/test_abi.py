@@ -62,6 +62,8 @@ def _unpack_plan_offsets(arch):
         Kp = (K + 15) // 16 * 16
         out[key] = (take(N * Kp), take(N), N, Kp)
         out[key + "/wx"] = take((3 * N * Kp + 1) // 2)  # bf16x6 terms [3][N][Kpad]
+        out[key + "/wh"] = take(N * Kp)                 # fp16x3 terms [2][N][Kpad]
+        out[key + "/winv"] = take(N)
 
     conv("stem", 64, 196)
     inpl = 64
@@ -123,6 +125,19 @@ def test_pack_weights_folds_batchnorm(golden):
         assert np.all(np.abs(f[1]) <= np.abs(f[0]) * 2.0 ** -8 + 1e-45)
         hi = (W.view(np.uint32) + 0x7FFF + ((W.view(np.uint32) >> 16) & 1)) >> 16
         np.testing.assert_array_equal(t[0], hi.astype(np.uint16))
+        # fp16x3: W[n] * 2^(13 - e[n]) = hi + lo (fp16, round to nearest even), winv = 2^(e - 13)
+        Wn = W.reshape(N, Kp)
+        winv = packed[offs[key + "/winv"]:offs[key + "/winv"] + N]
+        e = np.floor(np.log2(np.abs(Wn).max(1)))
+        np.testing.assert_array_equal(winv, np.exp2(e - 13).astype(np.float32))
+        x2 = offs[key + "/wh"]
+        hl = packed[x2:x2 + N * Kp].view(np.float16).reshape(2, N, Kp)
+        scaled = Wn * (1.0 / winv[:, None])
+        assert np.abs(scaled).max() < 2.0 ** 14
+        np.testing.assert_array_equal(hl[0], scaled.astype(np.float16))
+        np.testing.assert_array_equal(hl[1], (scaled - hl[0].astype(np.float32)).astype(np.float16))
+        rel = np.abs(hl[0].astype(np.float64) + hl[1] - scaled) / np.abs(scaled).max(1, keepdims=True)
+        assert rel.max() <= 2.0 ** -22  # 22 significand bits
 
 
 def test_pack_rejects_wrong_state():

@@ -18,6 +18,13 @@ pytestmark = pytest.mark.gpu
 
 TOL = 1e-4
 
+MATHS = ("f32", "bf16x6", "fp16x3")
+
+
+def _math(name):
+    from sfa_hip import _lib
+    return {"f32": _lib.MATH_F32, "bf16x6": _lib.MATH_BF16X6, "fp16x3": _lib.MATH_FP16X3}[name]
+
 
 class Cfg(dict):
     __getattr__ = dict.__getitem__
@@ -36,9 +43,13 @@ def _err(a, b):
     return float(np.max(np.abs(a - b) / np.maximum(1.0, np.abs(b))))
 
 
+@pytest.mark.parametrize("math", MATHS)
 @pytest.mark.parametrize("case", list(gc.MODEL_CASES))
-def test_forward_small_inputs(golden, gpu, case):
+def test_forward_small_inputs(golden, gpu, case, math):
+    """Small maps too: at 32..96 px a conv tile spans many frames (per-frame fp16x3 maxima
+    are then committed row by row, conv.h AmaxRows)."""
     model = make_model(golden, gpu)
+    model._engine(gpu).set_math(_math(math))
     x = torch.from_numpy(gc.model_input(case)).to(gpu)
     with torch.no_grad():
         out = model(x)
@@ -113,9 +124,12 @@ def test_forward_608_end_to_end(golden, gpu):
         assert abs(len(post[0][j]) - len(g[f"e2e/post_cls{j}"])) <= 1
 
 
-def test_batch_consistency(golden, gpu):
-    """Frame b of a batch == the same frame alone (no cross-frame leakage, bs=16 path)."""
+@pytest.mark.parametrize("math", MATHS)
+def test_batch_consistency(golden, gpu, math):
+    """Frame b of a batch == the same frame alone, bit for bit (no cross-frame leakage;
+    fp16x3 scales every frame by its own activation maxima)."""
     model = make_model(golden, gpu)
+    model._engine(gpu).set_math(_math(math))
     x = torch.from_numpy(synthetic.synthetic_bev(4, 160, 192, seed=5)).to(gpu)
     with torch.no_grad():
         full = model(x)
@@ -141,16 +155,16 @@ def test_cpu_input_raises(golden):
         model(torch.zeros(1, 3, 64, 64))
 
 
-@pytest.mark.parametrize("math", ["f32", "bf16x6"])
+@pytest.mark.parametrize("math", MATHS)
 def test_forward_608_math_modes(golden, gpu, math):
-    """Both convolution arithmetics (include/sfa_hip.h sfa_math) meet the logit bar on the
-    full-size frame; bf16x6 (default) is f32-accurate, not a reduced-precision mode."""
+    """Every convolution arithmetic (include/sfa_hip.h sfa_math) meets the logit bar on the
+    full-size frame; the split modes are f32-accurate, not reduced-precision modes."""
     from data_process.kitti_bev_utils import makeBEVMap
     from data_process.kitti_data_utils import get_filtered_lidar
     from sfa_hip import _lib
     model = make_model(golden, gpu)
     eng = model._engine(gpu)
-    eng.set_math(_lib.MATH_F32 if math == "f32" else _lib.MATH_BF16X6)
+    eng.set_math(_math(math))
     assert _lib.lib().sfa_model_get_math(eng._h) == eng.math
     cloud = synthetic.synthetic_point_cloud(1)
     x = torch.from_numpy(makeBEVMap(get_filtered_lidar(cloud, gc.BOUNDARY), gc.BOUNDARY)[None])

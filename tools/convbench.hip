@@ -81,6 +81,33 @@ static uint16_t* split_weights(const float* w, size_t n) {
   return d;
 }
 
+// [N][Kpad] f32 (device) -> fp16x3 terms [2][N][Kpad] of w * 2^(13 - e[n]) and winv[n]
+static void split_weights_h3(const float* w, int N, int Kpad, uint16_t** wh, float** winv) {
+  const size_t n = (size_t)N * Kpad;
+  std::vector<float> hw(n), inv(N);
+  CK(hipMemcpy(hw.data(), w, n * 4, hipMemcpyDeviceToHost));
+  std::vector<_Float16> hs(2 * n);
+  for (int o = 0; o < N; ++o) {
+    float mx = 0.f;
+    for (int k = 0; k < Kpad; ++k) mx = std::max(mx, std::fabs(hw[(size_t)o * Kpad + k]));
+    int e = 0;
+    if (mx > 0.f) (void)std::frexp(mx, &e), e -= 1;  // mx in [2^e, 2^(e+1))
+    const float sc = std::ldexp(1.f, 13 - e);
+    inv[o] = std::ldexp(1.f, e - 13);
+    for (int k = 0; k < Kpad; ++k) {
+      const size_t i = (size_t)o * Kpad + k;
+      const float x = hw[i] * sc;
+      const _Float16 hi = (_Float16)x;
+      hs[i] = hi;
+      hs[n + i] = (_Float16)(x - (float)hi);
+    }
+  }
+  CK(hipMalloc(wh, hs.size() * 2));
+  CK(hipMemcpy(*wh, hs.data(), hs.size() * 2, hipMemcpyHostToDevice));
+  CK(hipMalloc(winv, N * 4));
+  CK(hipMemcpy(*winv, inv.data(), N * 4, hipMemcpyHostToDevice));
+}
+
 struct Shape {
   const char* name;
   int B, H, W, C, k, stride, pad, N;
@@ -119,6 +146,16 @@ struct Cand {
     "x6g " #BM "x" #BN " w" #WM " occ" #OCC " abl" #ABL, 16,                              \
         [](const ConvArgs& a, hipStream_t s) { return launch_conv_x6g_cfg<BM, BN, WM, EPI, OCC, 16, 3, ABL>(a, s); } \
   }
+#define CANDH(BM, BN, WM, EPI, OCC)                                                      \
+  Cand {                                                                                \
+    "h3g " #BM "x" #BN " w" #WM " occ" #OCC, 16,                                          \
+        [](const ConvArgs& a, hipStream_t s) { return launch_conv_x6g_cfg<BM, BN, WM, EPI, OCC, 16, 3, 0, BN, 1>(a, s); } \
+  }
+#define CANDHK(BM, BN, WM, EPI, OCC, BK, NS)                                            \
+  Cand {                                                                                \
+    "h3g " #BM "x" #BN " w" #WM " occ" #OCC " bk" #BK " st" #NS, BK,                      \
+        [](const ConvArgs& a, hipStream_t s) { return launch_conv_x6g_cfg<BM, BN, WM, EPI, OCC, BK, NS, 0, BN, 1>(a, s); } \
+  }
 #define CANDA(BM, BN, WM, WN, BK, EPI, OCC, ABL) CANDG(BM, BN, WM, WN, BK, EPI, OCC, false, ABL)
 #define CAND(BM, BN, WM, WN, BK, EPI, OCC) CANDA(BM, BN, WM, WN, BK, EPI, OCC, 0)
 
@@ -137,18 +174,21 @@ int main(int argc, char** argv) {
   };
   std::vector<Cand> n64 = {
       CAND(128, 64, 32, 64, 16, EPI_STD, 4),
-      CANDXG(256, 64, 32, EPI_STD, 1), CANDXGK(128, 64, 32, EPI_STD, 2, 16, 2), CANDXGK(128, 64, 32, EPI_STD, 3, 16, 2),
-      CANDXGK(256, 64, 32, EPI_STD, 2, 16, 2),
+      CANDXG(256, 64, 32, EPI_STD, 1),
+      CANDH(256, 64, 32, EPI_STD, 1), CANDH(256, 64, 32, EPI_STD, 2), CANDH(128, 64, 32, EPI_STD, 2),
+      CANDHK(256, 64, 32, EPI_STD, 1, 32, 3), CANDHK(128, 64, 32, EPI_STD, 2, 32, 2),
   };
   std::vector<Cand> nbig = {
       CAND(64, 128, 32, 64, 16, EPI_STD, 4),
-      CANDXG(128, 128, 32, EPI_STD, 2), CANDXGK(128, 128, 32, EPI_STD, 2, 16, 2), CANDXGK(128, 256, 32, EPI_STD, 2, 16, 2),
-      CANDXGK(256, 128, 32, EPI_STD, 2, 16, 2),
+      CANDX(128, 128, 64, 64, 16, EPI_STD, 2), CANDXG(128, 128, 32, EPI_STD, 2), CANDX(64, 128, 32, 64, 32, EPI_STD, 2),
+      CANDH(128, 128, 32, EPI_STD, 2), CANDH(256, 128, 32, EPI_STD, 1), CANDH(64, 128, 32, EPI_STD, 2),
+      CANDHK(128, 128, 32, EPI_STD, 2, 32, 2), CANDHK(128, 128, 32, EPI_STD, 1, 32, 3),
   };
   std::vector<Cand> heads = {
       CAND(128, 64, 32, 64, 16, EPI_HEAD, 4),
-      CANDXG(256, 320, 32, EPI_HEAD, 1), CANDXGK(128, 320, 32, EPI_HEAD, 2, 16, 2),
-      CANDXGK(256, 320, 32, EPI_HEAD, 1, 16, 2),
+      CANDXG(256, 320, 32, EPI_HEAD, 1),
+      CANDH(256, 320, 32, EPI_HEAD, 1), CANDH(128, 320, 32, EPI_HEAD, 1),
+      CANDHK(256, 320, 32, EPI_HEAD, 1, 32, 2), CANDHK(128, 320, 32, EPI_HEAD, 1, 32, 2),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -162,7 +202,22 @@ int main(int argc, char** argv) {
     const int M = sh.B * OH * OW;
     const int K = sh.k * sh.k * sh.C;
     const int Kpad = (K + 31) / 32 * 32;
-    float* x = dev_random((size_t)sh.B * sh.H * sh.W * sh.C, 1, 1.0f);
+    const size_t nx = (size_t)sh.B * sh.H * sh.W * sh.C;
+    float* x = dev_random(nx, 1, 1.0f);
+    unsigned* amax_x;  // per-frame max |x| (conv.h fp16x3 layout)
+    {
+      std::vector<float> hx(nx);
+      CK(hipMemcpy(hx.data(), x, nx * 4, hipMemcpyDeviceToHost));
+      std::vector<unsigned> words((size_t)sh.B * SFA_AMAX_WORDS, 0u);
+      const size_t per = nx / sh.B;
+      for (int b = 0; b < sh.B; ++b) {
+        float mx = 0.f;
+        for (size_t i = 0; i < per; ++i) mx = std::max(mx, std::fabs(hx[b * per + i]));
+        memcpy(&words[(size_t)b * SFA_AMAX_WORDS + SFA_AMAX_STRIDE * 3], &mx, 4);
+      }
+      CK(hipMalloc(&amax_x, words.size() * 4));
+      CK(hipMemcpy(amax_x, words.data(), words.size() * 4, hipMemcpyHostToDevice));
+    }
     float* w = dev_random((size_t)sh.N * Kpad, 2, 2.0f / std::sqrt((float)K));
     float* b = dev_random(sh.N, 3, 0.2f);
     float* res = sh.res ? dev_random((size_t)M * sh.N, 4, 1.0f) : nullptr;
@@ -221,6 +276,12 @@ int main(int argc, char** argv) {
       }
       a.w = wv;
       a.wx = c.name.rfind("x6", 0) == 0 ? split_weights(wv, (size_t)sh.N * a.Kpad) : nullptr;
+      uint16_t* whp = nullptr;
+      float* winvp = nullptr;
+      if (c.name.rfind("h3", 0) == 0) split_weights_h3(wv, sh.N, a.Kpad, &whp, &winvp);
+      a.wh = whp;
+      a.winv = winvp;
+      a.amax_in[0] = whp ? amax_x : nullptr;
       a.y = y;
       a.hout = y;
       CK(hipMemset(y, 0, ysz * 4));
@@ -256,8 +317,11 @@ int main(int argc, char** argv) {
              flop / (med * 1e-3) / 1e12, maxd, maxr);
       if (wv != w) CK(hipFree(wv));
       if (a.wx) CK(hipFree(const_cast<uint16_t*>(a.wx)));
+      if (whp) CK(hipFree(whp));
+      if (winvp) CK(hipFree(winvp));
     }
     CK(hipFree(x));
+    CK(hipFree(amax_x));
     CK(hipFree(w));
     CK(hipFree(b));
     if (res) CK(hipFree(res));

@@ -24,12 +24,30 @@ def load(p):
 
 passes = [load(p) for p in sorted(d for d in os.listdir(base) if d.startswith("p") and
                                   os.path.isdir(os.path.join(base, d)))]
+# dispatches are matched across passes by (kernel, grid, occurrence): with the level-0
+# heads on a side stream the dispatch order differs from pass to pass
+def keyed(p):
+    seen = collections.Counter()
+    out = {}
+    for r in p:
+        k = (r["name"], r["grid"])
+        out[k + (seen[k],)] = r
+        seen[k] += 1
+    return out
+
+
+keyed_passes = [keyed(p) for p in passes[1:]]
 merged = []
-for i in range(min(len(p) for p in passes)):
-    row = dict(passes[0][i])
-    for p in passes[1:]:
-        assert p[i]["name"] == row["name"]
-        row.update({k: v for k, v in p[i].items() if k not in ("name", "grid", "dur_ns")})
+seen = collections.Counter()
+for r0 in passes[0]:
+    k = (r0["name"], r0["grid"])
+    key = k + (seen[k],)
+    seen[k] += 1
+    if not all(key in kp for kp in keyed_passes):
+        continue
+    row = dict(r0)
+    for kp in keyed_passes:
+        row.update({k2: v for k2, v in kp[key].items() if k2 not in ("name", "grid", "dur_ns")})
     merged.append(row)
 # last forward: from the last nchw3_to_nhwc4 dispatch to the following kfpn_combine
 starts = [i for i, r in enumerate(merged) if "nchw3_to_nhwc4" in r["name"]]
