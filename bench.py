@@ -444,8 +444,8 @@ def main():
                           "note": "one step in flight; value/ms_per_step use %d in flight" % nf},
             "roofline": {
                 "bound": "mfma",
-                "kernel": ("conv_mfma_kernel" if args.math == "f32" else
-                           "conv_x6_kernel / conv_x6g_kernel (math %s)" % args.math) +
+                "kernel": {"f32": "conv_mfma_kernel", "bf16x6": "conv_x6_kernel / conv_x6g_kernel",
+                           "fp16x3": "conv_h3_kernel"}.get(args.math, args.math) + " (math %s)" % args.math +
                           " (23 implicit-GEMM launches per forward; achieved = algorithmic f32 FLOP "
                           "over the whole forward's event time, aux kernels included)",
                 "achieved": round(achieved, 3),

@@ -2,6 +2,7 @@
 // configuration per layer shape (conv_kernel.h, conv_x6_kernel.h).
 #include "conv_kernel.h"
 #include "conv_x6_kernel.h"
+#include "conv_h3_kernel.h"
 
 namespace sfa {
 
@@ -28,30 +29,30 @@ static int launch_conv_x6(const ConvArgs& a, int epilogue, hipStream_t st) {
   return rc;
 }
 
-// fp16x3 tiles per shape (tools/convbench.hip, profiles/r01_convbench_h3.txt): BK = 32
-// with a 2-deep ring where K allows it (half the barriers per MAC), 256-row tiles for
-// the 64-wide and the big-M layers.  Returns SFA_E_UNSUPPORTED when no tile fits.
+// fp16x3 tiles per shape (tools/convbench.hip sweeps, profiles/r01_convbench_h3n.txt): the
+// streamlined conv_h3_kernel (fixed DMA slots per wave, pipelined fragment reads) with
+// BK = 32 and a 2-deep ring wherever K allows it, 256-row tiles for the heads and the
+// 7x7 stem (K = 196: BK 16); conv_x6g_kernel<..., PREC 1> tiles as the fallback.
 static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;
   auto ok = [](int rc) { return rc != SFA_E_UNSUPPORTED; };
   int rc = SFA_E_UNSUPPORTED;
   if (epilogue == EPI_HEAD) {
     if (a.N == 320) {
-      rc = launch_conv_x6g_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, 0, 320, 1>(a, st);
+      rc = launch_conv_h3_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, false, 6>(a, st);
       if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 320, 32, EPI_HEAD, 1, 16, 3, 0, 320, 1>(a, st);
     }
     if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_HEAD, 1, 16, 3, 0, 64, 1>(a, st);
     return rc;
   }
   if (a.N == 64) {
-    if (a.M >= 50000) rc = launch_conv_x6g_cfg<128, 64, 32, EPI_STD, 2, 32, 2, 0, 64, 1>(a, st);
+    if (a.Kpad >= 256) rc = launch_conv_h3_cfg<128, 64, 32, EPI_STD, 2, 32, 2, false, 0>(a, st);
+    if (!ok(rc)) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 16, 3, false, 0>(a, st);
     if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_STD, 1, 16, 3, 0, 64, 1>(a, st);
     return rc;
   }
   if (a.N % 128 == 0) {
-    if (a.M >= 50000) rc = launch_conv_x6g_cfg<256, 128, 32, EPI_STD, 1, 16, 3, 0, 128, 1>(a, st);
-    else if (a.M >= 10000) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2, 32, 2, 0, 128, 1>(a, st);
-    else rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 1, 32, 3, 0, 128, 1>(a, st);
+    rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(a, st);
     if (!ok(rc)) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2, 16, 3, 0, 128, 1>(a, st);
   }
   return rc;

@@ -1,0 +1,345 @@
+// Implicit-GEMM convolution, fp16x3 arithmetic, streamlined for gfx950 (CDNA4).
+//
+// Same GEMM view, operand split and epilogues as conv_x6g_kernel<..., PREC = 1>
+// (conv_x6_kernel.h): C[M][N] = A[M][K] * W[N][K]^T over NHWC, A (f32) gathered with
+// LDS-DMA and split into two fp16 terms (x s = hi + lo, s the frame's power-of-two
+// scale) when a wave reads its fragment, W pre-split on the host into two fp16 terms,
+// products hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_f16 with f32 accumulation.
+// What differs is the register and instruction budget around the MFMAs:
+//  * every wave owns a FIXED set of DMA slots per K-tile (NA A-row groups, NB W-row
+//    groups), so the per-row gather origins are NA (not NA + NB) registers and the W
+//    source offsets are precomputed (one add per tile);
+//  * the gather origin of a row is two registers per segment (pixel index; ih, iw packed
+//    as two int16), and the segment count is a template parameter (no dead copies);
+//  * the W fragments are read one column block ahead of the MFMAs that use them, and the
+//    A fragments of the next k-step are read and split between the current step's MFMAs;
+//  * NSTAGE-deep ring (prefetch distance NSTAGE - 1 tiles) and optional N-major tile order
+//    (all M-tiles of one weight column block on one XCD: weights larger than an XCD's L2).
+// LDS images (16-B quad/chunk q of row R stored at q ^ swz(R); conflict-free ds_read_b128):
+//   A rows BK f32:  BK 32 -> 128 B, swz (R >> 1) & 7;  BK 16 -> 64 B, swz (R >> 2) & 3
+//   W rows BK fp16: BK 32 ->  64 B, swz (R >> 2) & 3;  BK 16 -> 32 B, swz (R >> 3) & 1
+#pragma once
+
+#include "conv_x6_kernel.h"
+
+namespace sfa {
+
+// ABL (variants for tools/convbench): 1 = no DMA in the K loop (ablation), 2 = software-
+// pipelined fragment reads (compute_pipe), 4 = s_setprio 1 for the second half of the waves.
+template <int BM, int BN, int WM, int EPI, int OCC, int BK, int NSTAGE, int NSEG, bool NMAJ = false,
+          int ABL = 0>
+__global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const ConvArgs a) {
+  static_assert(BK == 16 || BK == 32, "BK");
+  static_assert(NSTAGE >= 2 && NSTAGE <= 4, "ring depth");
+  static_assert(NSEG == 1 || NSEG == 2, "segments");
+  constexpr int NW = BM / WM, NT = NW * 64;
+  constexpr int TM = WM / 32, TN = BN / 32;
+  constexpr int KST = BK / 16;
+  constexpr int AROW = BK * 4, BROW = BK * 2;  // bytes per LDS row
+  constexpr int A_BYTES = BM * AROW, TERM_B = BN * BROW;
+  constexpr int STAGE = A_BYTES + 2 * TERM_B;
+  constexpr int A_RPD = 1024 / AROW, B_RPD = 1024 / BROW;  // rows per DMA instruction
+  constexpr int ND_A = BM / A_RPD, ND_BT = BN / B_RPD, ND_B = 2 * ND_BT;
+  static_assert(BM % A_RPD == 0 && BN % B_RPD == 0 && BN % 32 == 0 && WM % 32 == 0, "tile");
+  static_assert(ND_A % NW == 0, "A DMA groups per wave");
+  constexpr int NA = ND_A / NW;
+  constexpr int NB = (ND_B + NW - 1) / NW;
+  constexpr int NB_REM = ND_B % NW;  // if != 0: waves < NB_REM issue NB W DMAs, the rest NB - 1
+  constexpr int HCH = BM < 128 ? BM : 128;
+  constexpr int HEAD_BYTES = EPI == EPI_HEAD ? HCH * 65 * 4 : 0;
+  constexpr int LDS_BYTES = NSTAGE * STAGE > HEAD_BYTES ? NSTAGE * STAGE : HEAD_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+
+  auto swzA = [](int R) { return BK == 16 ? ((R >> 2) & 3) : ((R >> 1) & 7); };
+  auto swzB = [](int R) { return BK == 16 ? ((R >> 3) & 1) : ((R >> 2) & 3); };
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n_tiles = a.N / BN;
+  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  int mt, nt;
+  if constexpr (NMAJ) {
+    const int m_tiles = (a.M + BM - 1) / BM;
+    nt = lbid / m_tiles;
+    mt = lbid - nt * m_tiles;
+  } else {
+    mt = lbid / n_tiles;
+    nt = lbid - mt * n_tiles;
+  }
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int M = a.M;
+
+  // ---- A DMA slots: groups d = wave + NW * i, rows A_RPD * d + lane / QPR ----
+  constexpr int QPR = AROW / 16;
+  const int arow_in = lane / QPR;
+  // the lane's logical f32 quad: every slot's row has the same swizzle (BK 16: A_RPD = 16;
+  // BK 32: rows 8d + lane/8 with d of the wave's parity, NW even)
+  static_assert(BK == 16 || NW % 2 == 0, "swizzle period");
+  const int kq = (lane % QPR) ^ swzA(A_RPD * wave + arow_in);
+  int r_pix[NSEG][NA], r_ihw[NSEG][NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int m = m0 + A_RPD * (wave + NW * i) + arow_in;
+    const bool ok = m < M;
+    const int mm = ok ? m : 0;
+    const int ow = mm % a.OW;
+    const int t = mm / a.OW;
+    const int oh = t % a.OH;
+    const int b = t / a.OH;
+#pragma unroll
+    for (int sg = 0; sg < NSEG; ++sg) {
+      const ConvSeg& g = a.seg[sg];
+      const int ih = ok ? oh * g.stride - g.pad : -16384;
+      const int iw = ow * g.stride - g.pad;
+      r_pix[sg][i] = (b * g.H + ih) * g.W + iw;
+      r_ihw[sg][i] = (ih << 16) | (iw & 0xffff);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.seg[0].x), (short)0, (int)a.seg[0].bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.seg[NSEG - 1].x), (short)0, (int)a.seg[NSEG - 1].bytes, 0x00020000);
+
+  // ---- W DMA slots: groups e = wave + NW * j (term e / ND_BT, rows (e % ND_BT) * B_RPD + ..) ----
+  const unsigned term_bytes = (unsigned)a.N * (unsigned)a.Kpad * 2u;
+  const __amdgpu_buffer_rsrc_t rsw =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.wh), (short)0, (int)(2 * term_bytes), 0x00020000);
+  constexpr int CPR = BROW / 16;
+  int boff[NB];  // int array + unsigned cast at the use: other forms make hipcc's host pass drop the kernel stub
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int e = wave + NW * j < ND_B ? wave + NW * j : ND_B - 1;
+    const int t = e / ND_BT;
+    const int R = (e % ND_BT) * B_RPD + lane / CPR;
+    const int lc = (lane % CPR) ^ swzB(R);
+    boff[j] = (int)(t * term_bytes) + (int)(((n0 + R) * a.Kpad + 8 * lc) << 1);
+  }
+
+  // fp16x3 scale of the frame of this lane's A row in each 32-row MFMA tile
+  float as[TM], ainv[TM];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+    const int m = min(m0 + wave * WM + mi * 32 + (lane & 31), M - 1);
+    as[mi] = amax_frame_scale(a.amax_in, NSEG, m / (a.OH * a.OW), ainv[mi]);
+  }
+
+  auto load_a = [&](auto sgc, const __amdgpu_buffer_rsrc_t rs, int kl, unsigned char* S) {
+    constexpr int SG = decltype(sgc)::value;
+    const ConvSeg& g = a.seg[SG];
+    const int kk = kl + 4 * kq;
+    const int tap = kk >> g.logC;
+    const int c = kk & (g.C - 1);
+    const int kh = (tap * g.kdiv_mul) >> g.kdiv_sh;
+    const int kw = tap - kh * g.KW;
+    const bool tap_ok = tap < g.taps;
+    const int toff = kh * g.W + kw;
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int ih = r_ihw[SG][i] >> 16;
+      const int iw = (int)(short)(r_ihw[SG][i] & 0xffff);
+      const bool ok = tap_ok & ((unsigned)(ih + kh) < (unsigned)g.H) & ((unsigned)(iw + kw) < (unsigned)g.W);
+      const unsigned off = ok ? (unsigned)((((r_pix[SG][i] + toff) << g.logC) + c) << 2) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(S + (wave + NW * i) * 1024), 16, off, 0, 0, 0);
+    }
+  };
+  auto load_tile = [&](int kt, unsigned char* S) {
+    const int k0 = kt * BK;
+    if constexpr (NSEG == 2) {
+      if (k0 >= a.kseg1)
+        load_a(std::integral_constant<int, 1>(), rs1, k0 - a.kseg1, S);
+      else
+        load_a(std::integral_constant<int, 0>(), rs0, k0, S);
+    } else {
+      load_a(std::integral_constant<int, 0>(), rs0, k0, S);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (NB_REM == 0 || j < NB - 1 || wave < NB_REM)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsw, (__attribute__((address_space(3))) void*)(S + A_BYTES + (wave + NW * j) * 1024), 16,
+            (unsigned)(boff[j] + 2 * k0), 0, 0, 0);
+    }
+  };
+
+  x6_f32x16 acc[TM][TN];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[mi][ni][v] = 0.f;
+
+  const int r = lane & 31, h = lane >> 5;
+  // per-lane LDS byte offsets (stage-relative)
+  int aoff[TM][2 * KST];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+    const int R = wave * WM + mi * 32 + r;
+#pragma unroll
+    for (int q = 0; q < 2 * KST; ++q) aoff[mi][q] = R * AROW + ((((q >> 1) * 4 + 2 * h + (q & 1)) ^ swzA(R)) << 4);
+  }
+  int bbase[KST];
+#pragma unroll
+  for (int s = 0; s < KST; ++s) bbase[s] = A_BYTES + r * BROW + (((2 * s + h) ^ swzB(r)) << 4);
+
+  auto read_a = [&](const unsigned char* S, int s, f16x8_t (&hf)[2][TM]) {
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const x6_f32x4 q0 = *reinterpret_cast<const x6_f32x4*>(S + aoff[mi][2 * s]);
+      const x6_f32x4 q1 = *reinterpret_cast<const x6_f32x4*>(S + aoff[mi][2 * s + 1]);
+      f16x4_t t0, t1, u0, u1;
+      split2h(q0, as[mi], t0, t1);
+      split2h(q1, as[mi], u0, u1);
+      hf[0][mi] = __builtin_shufflevector(t0, u0, 0, 1, 2, 3, 4, 5, 6, 7);
+      hf[1][mi] = __builtin_shufflevector(t1, u1, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  };
+  auto compute = [&](const unsigned char* S) {
+#pragma unroll
+    for (int s = 0; s < KST; ++s) {
+      f16x8_t hf[2][TM];
+      read_a(S, s, hf);
+      const unsigned char* SB = S + bbase[s];
+      f16x8_t b0 = *reinterpret_cast<const f16x8_t*>(SB);
+      f16x8_t b1 = *reinterpret_cast<const f16x8_t*>(SB + TERM_B);
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        f16x8_t c0 = b0, c1 = b1;
+        if (ni + 1 < TN) {  // next column block's fragments, one block ahead of their MFMAs
+          b0 = *reinterpret_cast<const f16x8_t*>(SB + (ni + 1) * 32 * BROW);
+          b1 = *reinterpret_cast<const f16x8_t*>(SB + TERM_B + (ni + 1) * 32 * BROW);
+        }
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) {
+          x6_f32x16 cc = acc[mi][ni];
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(hf[1][mi], c0, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(hf[0][mi], c1, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(hf[0][mi], c0, cc, 0, 0, 0);
+          acc[mi][ni] = cc;
+        }
+      }
+    }
+  };
+
+  // Software-pipelined form (ABL & 2): the scheduler may not move instructions across
+  // the column-block boundaries, so the W fragments are read two column blocks ahead
+  // (across the k-step boundary too) and the next k-step's A quads are read after the
+  // first column block and split after the third, between MFMAs.
+  auto compute_pipe = [&](const unsigned char* S) {
+    constexpr int NSTEP = KST * TN;  // (k-step, column block) pairs in program order
+    f16x8_t bq[3][2];                // W fragment ring: pair p lives in slot p % 3
+    x6_f32x4 qa[TM][2];
+    f16x8_t hf[2][TM], hn[2][TM];
+    auto read_b = [&](int p) {
+      const int s = p / TN, ni = p % TN;
+      const unsigned char* SB = S + bbase[s] + ni * 32 * BROW;
+      bq[p % 3][0] = *reinterpret_cast<const f16x8_t*>(SB);
+      bq[p % 3][1] = *reinterpret_cast<const f16x8_t*>(SB + TERM_B);
+    };
+    auto read_qa = [&](int s) {
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        qa[mi][0] = *reinterpret_cast<const x6_f32x4*>(S + aoff[mi][2 * s]);
+        qa[mi][1] = *reinterpret_cast<const x6_f32x4*>(S + aoff[mi][2 * s + 1]);
+      }
+    };
+    auto split_qa = [&](f16x8_t (&dst)[2][TM]) {
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        f16x4_t t0, t1, u0, u1;
+        split2h(qa[mi][0], as[mi], t0, t1);
+        split2h(qa[mi][1], as[mi], u0, u1);
+        dst[0][mi] = __builtin_shufflevector(t0, u0, 0, 1, 2, 3, 4, 5, 6, 7);
+        dst[1][mi] = __builtin_shufflevector(t1, u1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+    };
+    read_qa(0);
+    read_b(0);
+    if (NSTEP > 1) read_b(1);
+    split_qa(hf);
+#pragma unroll
+    for (int p = 0; p < NSTEP; ++p) {
+      const int s = p / TN, ni = p % TN;
+      if (p + 2 < NSTEP) read_b(p + 2);
+      if (s + 1 < KST && ni == 0) read_qa(s + 1);
+      if (s + 1 < KST && ni == (TN > 2 ? 2 : TN - 1)) split_qa(hn);
+      const f16x8_t c0 = bq[p % 3][0], c1 = bq[p % 3][1];
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        x6_f32x16 cc = acc[mi][ni];
+        cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(hf[1][mi], c0, cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(hf[0][mi], c1, cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(hf[0][mi], c0, cc, 0, 0, 0);
+        acc[mi][ni] = cc;
+      }
+      if (ni == TN - 1 && s + 1 < KST) {
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) {
+          hf[0][mi] = hn[0][mi];
+          hf[1][mi] = hn[1][mi];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  const int nk = a.Kpad / BK;
+  // ring: tile kt lives in stage kt % NSTAGE; tiles kt+1 .. kt+NSTAGE-1 are in flight
+#pragma unroll
+  for (int p = 0; p < NSTAGE - 1; ++p) load_tile(p < nk ? p : nk - 1, smem + p * STAGE);
+  if constexpr ((ABL & 4) != 0) {
+    if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  }
+  int st_cur = 0, st_next = NSTAGE - 1;
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's DMAs of tile kt have landed (later tiles' may still be in flight)
+    constexpr int PER = NA + NB;
+    if (NB_REM == 0 || wave < NB_REM)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * PER) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NSTAGE - 2) * (PER - 1)) : "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's: stage kt complete; stage kt-1 no longer read
+    if constexpr (!(ABL & 1)) {
+      const int kn = kt + NSTAGE - 1;
+      load_tile(kn < nk ? kn : nk - 1, smem + st_next * STAGE);
+    }
+    if constexpr ((ABL & 2) != 0)
+      compute_pipe(smem + st_cur * STAGE);
+    else
+      compute(smem + st_cur * STAGE);
+    st_cur = st_cur + 1 == NSTAGE ? 0 : st_cur + 1;
+    st_next = st_next + 1 == NSTAGE ? 0 : st_next + 1;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  x6_epilogue<BM, BN, WM, BN, TM, TN, NT, EPI, 1>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
+}
+
+template <int BM, int BN, int WM, int EPI, int OCC, int BK, int NSTAGE, bool NMAJ = false, int ABL = 0>
+inline int launch_conv_h3_cfg(const ConvArgs& a, hipStream_t st) {
+  if (!a.wh || !a.winv || a.Kpad % BK != 0 || (a.nseg == 2 && a.kseg1 % BK != 0) || a.N % BN != 0) {
+    set_error("conv_h3: K/N not aligned to the tile or no split weights (Kpad=%d kseg1=%d N=%d)", a.Kpad,
+              a.kseg1, a.N);
+    return SFA_E_UNSUPPORTED;
+  }
+  if (2ull * a.N * a.Kpad * 2ull >= (1ull << 31)) {
+    set_error("conv_h3: split weights >= 2 GiB");
+    return SFA_E_UNSUPPORTED;
+  }
+  const long long nblocks = (long long)ceil_div(a.M, BM) * (a.N / BN);
+  if (nblocks <= 0 || nblocks > 0x7fffffffll) {
+    set_error("conv_h3: bad grid (M=%d N=%d)", a.M, a.N);
+    return SFA_E_INVALID;
+  }
+  if (a.nseg == 2)
+    hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 2, NMAJ, ABL>), dim3((unsigned)nblocks),
+                       dim3((BM / WM) * 64), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 1, NMAJ, ABL>), dim3((unsigned)nblocks),
+                       dim3((BM / WM) * 64), 0, st, a);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+}  // namespace sfa

@@ -353,7 +353,8 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_x6_kerne
 // its own with a counted vmcnt, then the barrier makes the whole stage visible.
 // ABL: diagnostic ablation bits for tools/convbench (0 in the product): 1 = no DMA in
 // the K loop, 2 = no A split (raw bits as terms), 4 = W fragments read once per k-step
-// group instead of per column block, 8 = no barrier.
+// group instead of per column block, 8 = no barrier, 16 = no epilogue (one sum per lane
+// stored), 64 = s_setprio 1 for the second half of the waves (the SIMD partners).
 // PREC 1: the fp16x3 form (two fp16 W terms, scaled A split into two fp16 terms when read,
 // products hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_f16).
 template <int BM, int BN, int WM, int EPI, int OCC, int BK = 16, int NSTAGE = 3, int ABL = 0,
@@ -581,6 +582,9 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WNT) * 64, OCC) conv_x6g_ker
   };
 
   const int nk = a.Kpad / BK;
+  if constexpr ((ABL & 64) != 0) {
+    if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  }
   if constexpr (NSTAGE == 3) {
     load_tile(0, smem);
     load_tile(nk > 1 ? 1 : 0, smem + STAGE);
@@ -598,12 +602,23 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WNT) * 64, OCC) conv_x6g_ker
     load_tile(0, smem);
     for (int kt = 0; kt < nk; ++kt) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // tile kt landed (this wave)
-      __builtin_amdgcn_s_barrier();  // every wave: stage kt & 1 complete, stage (kt+1) & 1 free
-      load_tile(kt + 1 < nk ? kt + 1 : nk - 1, smem + ((kt + 1) & 1) * STAGE);
+      if constexpr (!(ABL & 8)) __builtin_amdgcn_s_barrier();  // every wave: stage kt & 1 complete, stage (kt+1) & 1 free
+      if constexpr (!(ABL & 1)) load_tile(kt + 1 < nk ? kt + 1 : nk - 1, smem + ((kt + 1) & 1) * STAGE);
       compute(smem + (kt & 1) * STAGE);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr ((ABL & 16) != 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) t += acc[mi][ni][v];
+    a.y[(size_t)blockIdx.x * NT + tid] = t;
+    return;
+  }
   __syncthreads();
   x6_epilogue<BM, BN, WM, WN, TM, TN, NT, EPI, PREC>(a, acc, smem, m0, n0, nt, wm, wn, tid, ainv);
 }

@@ -15,6 +15,7 @@
 
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_x6_kernel.h"
+#include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3_kernel.h"
 
 namespace sfa {
 void set_error(const char* fmt, ...) {
@@ -156,6 +157,16 @@ struct Cand {
     "h3g " #BM "x" #BN " w" #WM " occ" #OCC " bk" #BK " st" #NS, BK,                      \
         [](const ConvArgs& a, hipStream_t s) { return launch_conv_x6g_cfg<BM, BN, WM, EPI, OCC, BK, NS, 0, BN, 1>(a, s); } \
   }
+#define CANDHA(BM, BN, WM, EPI, OCC, BK, NS, ABL)                                     \
+  Cand {                                                                                \
+    "h3g " #BM "x" #BN " w" #WM " occ" #OCC " bk" #BK " st" #NS " abl" #ABL, BK,          \
+        [](const ConvArgs& a, hipStream_t s) { return launch_conv_x6g_cfg<BM, BN, WM, EPI, OCC, BK, NS, ABL, BN, 1>(a, s); } \
+  }
+#define CANDN(BM, BN, WM, EPI, OCC, BK, NS, NMAJ, ABL)                                \
+  Cand {                                                                                \
+    "h3n " #BM "x" #BN " w" #WM " occ" #OCC " bk" #BK " st" #NS " nmaj" #NMAJ " abl" #ABL, BK, \
+        [](const ConvArgs& a, hipStream_t s) { return launch_conv_h3_cfg<BM, BN, WM, EPI, OCC, BK, NS, NMAJ, ABL>(a, s); } \
+  }
 #define CANDA(BM, BN, WM, WN, BK, EPI, OCC, ABL) CANDG(BM, BN, WM, WN, BK, EPI, OCC, false, ABL)
 #define CAND(BM, BN, WM, WN, BK, EPI, OCC) CANDA(BM, BN, WM, WN, BK, EPI, OCC, 0)
 
@@ -177,18 +188,27 @@ int main(int argc, char** argv) {
       CANDXG(256, 64, 32, EPI_STD, 1),
       CANDH(256, 64, 32, EPI_STD, 1), CANDH(256, 64, 32, EPI_STD, 2), CANDH(128, 64, 32, EPI_STD, 2),
       CANDHK(256, 64, 32, EPI_STD, 1, 32, 3), CANDHK(128, 64, 32, EPI_STD, 2, 32, 2),
+      CANDN(128, 64, 32, EPI_STD, 2, 32, 2, false, 0), CANDN(256, 64, 32, EPI_STD, 1, 16, 3, false, 0),
+      CANDN(128, 64, 32, EPI_STD, 2, 32, 2, false, 2), CANDN(256, 64, 32, EPI_STD, 1, 16, 3, false, 2),
   };
   std::vector<Cand> nbig = {
       CAND(64, 128, 32, 64, 16, EPI_STD, 4),
       CANDX(128, 128, 64, 64, 16, EPI_STD, 2), CANDXG(128, 128, 32, EPI_STD, 2), CANDX(64, 128, 32, 64, 32, EPI_STD, 2),
       CANDH(128, 128, 32, EPI_STD, 2), CANDH(256, 128, 32, EPI_STD, 1), CANDH(64, 128, 32, EPI_STD, 2),
       CANDHK(128, 128, 32, EPI_STD, 2, 32, 2), CANDHK(128, 128, 32, EPI_STD, 1, 32, 3),
+      CANDN(256, 128, 32, EPI_STD, 1, 16, 3, false, 0), CANDN(256, 128, 32, EPI_STD, 1, 32, 2, false, 0),
+      CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 0), CANDN(128, 128, 32, EPI_STD, 1, 32, 3, false, 0),
+      CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2), CANDN(128, 128, 32, EPI_STD, 1, 32, 3, false, 2),
+      CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 4), CANDN(256, 128, 32, EPI_STD, 1, 16, 3, false, 2),
   };
   std::vector<Cand> heads = {
       CAND(128, 64, 32, 64, 16, EPI_HEAD, 4),
       CANDXG(256, 320, 32, EPI_HEAD, 1),
       CANDH(256, 320, 32, EPI_HEAD, 1), CANDH(128, 320, 32, EPI_HEAD, 1),
       CANDHK(256, 320, 32, EPI_HEAD, 1, 32, 2), CANDHK(128, 320, 32, EPI_HEAD, 1, 32, 2),
+      CANDN(256, 320, 32, EPI_HEAD, 1, 32, 2, false, 0), CANDN(256, 320, 32, EPI_HEAD, 1, 16, 3, false, 0),
+      CANDN(256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2), CANDN(256, 320, 32, EPI_HEAD, 1, 32, 2, false, 4),
+      CANDN(256, 320, 32, EPI_HEAD, 1, 32, 2, false, 6), CANDN(256, 320, 32, EPI_HEAD, 1, 16, 3, false, 2),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
