@@ -29,24 +29,25 @@ static int launch_conv_x6(const ConvArgs& a, int epilogue, hipStream_t st) {
   return rc;
 }
 
-// fp16x3 tiles per shape (tools/convbench.hip sweeps, profiles/r01_convbench_h3n.txt): the
-// streamlined conv_h3_kernel (fixed DMA slots per wave, pipelined fragment reads) with
-// BK = 32 and a 2-deep ring wherever K allows it, 256-row tiles for the heads and the
-// 7x7 stem (K = 196: BK 16); conv_x6g_kernel<..., PREC 1> tiles as the fallback.
+// fp16x3 tiles per shape (tools/convbench.hip sweeps, profiles/r01_convbench_h3n*.txt,
+// r01_convbench_h3m.txt): the streamlined conv_h3_kernel (fixed DMA slots per wave, pipelined
+// fragment reads) with BK = 32 and a 2-deep ring wherever K allows it; 16x16x32 MFMAs for the
+// heads and the 64-wide layers (-1.5 % / -11 %), 32x32x16 for the 128..512-wide ones; the 7x7
+// stem (K = 196) on BK 16; conv_x6g_kernel<..., PREC 1> tiles as the fallback.
 static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;
   auto ok = [](int rc) { return rc != SFA_E_UNSUPPORTED; };
   int rc = SFA_E_UNSUPPORTED;
   if (epilogue == EPI_HEAD) {
     if (a.N == 320) {
-      rc = launch_conv_h3_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, false, 6>(a, st);
+      rc = launch_conv_h3_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2, 1>(a, st);
       if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 320, 32, EPI_HEAD, 1, 16, 3, 0, 320, 1>(a, st);
     }
     if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_HEAD, 1, 16, 3, 0, 64, 1>(a, st);
     return rc;
   }
   if (a.N == 64) {
-    if (a.Kpad >= 256) rc = launch_conv_h3_cfg<128, 64, 32, EPI_STD, 2, 32, 2, false, 0>(a, st);
+    if (a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
     if (!ok(rc)) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 16, 3, false, 0>(a, st);
     if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_STD, 1, 16, 3, 0, 64, 1>(a, st);
     return rc;

@@ -24,16 +24,111 @@
 
 namespace sfa {
 
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+
+// Epilogue of the 16x16x32 form (accumulator layout of v_mfma_f32_16x16x32_f16: lane l,
+// register v -> row 4 (l >> 4) + v, column l & 15 of its 16x16 tile).  Same semantics as
+// x6_epilogue<..., PREC = 1>: scale back by 1/s of the row's frame and winv[n], bias,
+// residual, ReLU, store, per-frame max |y|; EPI_HEAD stages ReLU(conv3x3 + b) of each head
+// in LDS and applies its 1x1 conv, channel-planar out.
+template <int BM, int BN, int WM, int TM, int TN, int NT, int EPI>
+__device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
+                                              int m0, int n0, int nt, int wave, int tid,
+                                              const float (&ainv)[TM]) {
+  constexpr int HCH = BM < 128 ? BM : 128;
+  const int M = a.M, lane = tid & 63, c16 = lane & 15, g = lane >> 4;
+  float rinv[TM][4];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) rinv[mi][v] = __shfl(ainv[mi], 4 * g + v, 64);
+  if constexpr (EPI == EPI_STD) {
+    AmaxRows am(a.OH * a.OW, m0);
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      const int n = n0 + ni * 16 + c16;
+      const float bn = a.bias[n];
+      const float cs = a.winv[n];
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int m = m0 + wave * WM + mi * 16 + 4 * g + v;
+          if (m < M) {
+            float val = acc[mi][ni][v] * rinv[mi][v] * cs + bn;
+            if (a.res) val += a.res[(size_t)m * a.N + n];
+            if (a.relu) val = fmaxf(val, 0.f);
+            a.y[(size_t)m * a.N + n] = val;
+            if (a.amax_out) am.add(a.amax_out, m, val);
+          }
+        }
+      }
+    }
+    if (a.amax_out)
+      amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1, reinterpret_cast<float*>(smem));
+  } else {
+    static_assert(BN % 64 == 0, "whole heads per block");
+    constexpr int HPB = BN / 64;
+    float* T = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int hh = 0; hh < HPB; ++hh) {
+      const int head = nt * HPB + hh;
+      int ch = 0, hoff = 0;
+#pragma unroll
+      for (int j = 0; j < SFA_MAX_HEADS; ++j)
+        if (j == head) {
+          ch = a.hch[j];
+          hoff = a.hoff[j];
+        }
+#pragma unroll
+      for (int c0 = 0; c0 < BM; c0 += HCH) {
+#pragma unroll
+        for (int ni = 4 * hh; ni < 4 * hh + 4; ++ni) {
+          const int col = (ni - 4 * hh) * 16 + c16;  // column within the head
+          const float bn = a.bias[n0 + 64 * hh + col];
+          const float cs = a.winv[n0 + 64 * hh + col];
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const int row = wave * WM + mi * 16 + 4 * g + v - c0;
+              if (row >= 0 && row < HCH) T[row * 65 + col] = fmaxf(acc[mi][ni][v] * rinv[mi][v] * cs + bn, 0.f);
+            }
+        }
+        __syncthreads();
+        for (int idx = tid; idx < HCH * ch; idx += NT) {
+          const int row = idx % HCH, c = idx / HCH;
+          const int m = m0 + c0 + row;
+          if (m >= M) continue;
+          const float* wr = a.hw1 + (head * 4 + c) * 64;
+          float sum = a.hb1[head * 4 + c];
+          const float* tr = T + row * 65;
+#pragma unroll 16
+          for (int k = 0; k < 64; ++k) sum = fmaf(tr[k], wr[k], sum);
+          a.hout[(size_t)(hoff + c) * M + m] = sum;
+        }
+        __syncthreads();
+      }
+    }
+  }
+}
+
 // ABL (variants for tools/convbench): 1 = no DMA in the K loop (ablation), 2 = software-
 // pipelined fragment reads (compute_pipe), 4 = s_setprio 1 for the second half of the waves.
+// MF: 0 = v_mfma_f32_32x32x16_f16 (32-row / 32-column wave sub-tiles), 1 = v_mfma_f32_16x16x32_f16
+// (16 x 16 sub-tiles, BK 32: same LDS reads and registers per MAC; the chip holds a higher
+// clock under the 16x16 shape on random data, MI355X_MICROARCH.md 'DVFS give-back' (7)).
 template <int BM, int BN, int WM, int EPI, int OCC, int BK, int NSTAGE, int NSEG, bool NMAJ = false,
-          int ABL = 0>
+          int ABL = 0, int MF = 0>
 __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const ConvArgs a) {
   static_assert(BK == 16 || BK == 32, "BK");
   static_assert(NSTAGE >= 2 && NSTAGE <= 4, "ring depth");
   static_assert(NSEG == 1 || NSEG == 2, "segments");
+  static_assert(MF == 0 || (BK == 32 && WM % 16 == 0), "16x16x32 form: BK 32");
   constexpr int NW = BM / WM, NT = NW * 64;
-  constexpr int TM = WM / 32, TN = BN / 32;
+  constexpr int MT = MF ? 16 : 32;  // MFMA sub-tile edge
+  constexpr int TM = WM / MT, TN = BN / MT;
   constexpr int KST = BK / 16;
   constexpr int AROW = BK * 4, BROW = BK * 2;  // bytes per LDS row
   constexpr int A_BYTES = BM * AROW, TERM_B = BN * BROW;
@@ -50,8 +145,14 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
   constexpr int LDS_BYTES = NSTAGE * STAGE > HEAD_BYTES ? NSTAGE * STAGE : HEAD_BYTES;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
 
-  auto swzA = [](int R) { return BK == 16 ? ((R >> 2) & 3) : ((R >> 1) & 7); };
-  auto swzB = [](int R) { return BK == 16 ? ((R >> 3) & 1) : ((R >> 2) & 3); };
+  // 16x16x32 reads: lane l takes row l & 15, quads / chunk by l >> 4; the extra XOR terms
+  // make the ds_read_b128 lane groups {0-3,12-15,20-27}, ... hit 16 distinct bank quads
+  auto swzA = [](int R) {
+    return MF ? (((R >> 1) & 7) ^ (((R & 15) + 4) >> 2 & 2)) : (BK == 16 ? ((R >> 2) & 3) : ((R >> 1) & 7));
+  };
+  auto swzB = [](int R) {
+    return MF ? (((R >> 2) & 3) ^ ((((R & 15) + 4) >> 3) & 1)) : (BK == 16 ? ((R >> 3) & 1) : ((R >> 2) & 3));
+  };
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -119,7 +220,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
   float as[TM], ainv[TM];
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi) {
-    const int m = min(m0 + wave * WM + mi * 32 + (lane & 31), M - 1);
+    const int m = min(m0 + wave * WM + mi * MT + (lane & (MT - 1)), M - 1);
     as[mi] = amax_frame_scale(a.amax_in, NSEG, m / (a.OH * a.OW), ainv[mi]);
   }
 
@@ -162,13 +263,14 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
     }
   };
 
-  x6_f32x16 acc[TM][TN];
+  typedef typename std::conditional<MF == 1, f32x4_t, x6_f32x16>::type acc_t;
+  acc_t acc[TM][TN];
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) acc[mi][ni][v] = 0.f;
+      for (int v = 0; v < (MF ? 4 : 16); ++v) acc[mi][ni][v] = 0.f;
 
   const int r = lane & 31, h = lane >> 5;
   // per-lane LDS byte offsets (stage-relative)
@@ -196,6 +298,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
     }
   };
   auto compute = [&](const unsigned char* S) {
+    if constexpr (MF == 0) {
 #pragma unroll
     for (int s = 0; s < KST; ++s) {
       f16x8_t hf[2][TM];
@@ -220,6 +323,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
         }
       }
     }
+    }
   };
 
   // Software-pipelined form (ABL & 2): the scheduler may not move instructions across
@@ -227,6 +331,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
   // (across the k-step boundary too) and the next k-step's A quads are read after the
   // first column block and split after the third, between MFMAs.
   auto compute_pipe = [&](const unsigned char* S) {
+    if constexpr (MF == 0) {
     constexpr int NSTEP = KST * TN;  // (k-step, column block) pairs in program order
     f16x8_t bq[3][2];                // W fragment ring: pair p lives in slot p % 3
     x6_f32x4 qa[TM][2];
@@ -282,6 +387,49 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
       }
       __builtin_amdgcn_sched_barrier(0);
     }
+    }
+  };
+
+  // 16x16x32 form (one k-step per BK 32 tile): W fragments two column blocks ahead, as
+  // compute_pipe; lane l reads A row l & 15 quads 2 (l >> 4), +1 and W row l & 15 chunk l >> 4.
+  auto compute16 = [&](const unsigned char* S) {
+    if constexpr (MF == 1) {
+      const int c16 = lane & 15, g = lane >> 4;
+      f16x8_t hf[2][TM];
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        const int R = wave * WM + mi * 16 + c16;
+        const x6_f32x4 q0 = *reinterpret_cast<const x6_f32x4*>(S + R * AROW + (((2 * g) ^ swzA(R)) << 4));
+        const x6_f32x4 q1 = *reinterpret_cast<const x6_f32x4*>(S + R * AROW + (((2 * g + 1) ^ swzA(R)) << 4));
+        f16x4_t t0, t1, u0, u1;
+        split2h(q0, as[mi], t0, t1);
+        split2h(q1, as[mi], u0, u1);
+        hf[0][mi] = __builtin_shufflevector(t0, u0, 0, 1, 2, 3, 4, 5, 6, 7);
+        hf[1][mi] = __builtin_shufflevector(t1, u1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+      const unsigned char* SB = S + A_BYTES + c16 * BROW + ((g ^ swzB(c16)) << 4);
+      f16x8_t bq[3][2];
+      auto read_b = [&](int ni) {
+        bq[ni % 3][0] = *reinterpret_cast<const f16x8_t*>(SB + ni * 16 * BROW);
+        bq[ni % 3][1] = *reinterpret_cast<const f16x8_t*>(SB + TERM_B + ni * 16 * BROW);
+      };
+      read_b(0);
+      if (TN > 1) read_b(1);
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        if (ni + 2 < TN) read_b(ni + 2);
+        const f16x8_t c0 = bq[ni % 3][0], c1 = bq[ni % 3][1];
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) {
+          f32x4_t cc = acc[mi][ni];
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[1][mi], c0, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c1, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c0, cc, 0, 0, 0);
+          acc[mi][ni] = cc;
+        }
+        if constexpr ((ABL & 2) != 0) __builtin_amdgcn_sched_barrier(0);
+      }
+    }
   };
 
   const int nk = a.Kpad / BK;
@@ -304,7 +452,9 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
       const int kn = kt + NSTAGE - 1;
       load_tile(kn < nk ? kn : nk - 1, smem + st_next * STAGE);
     }
-    if constexpr ((ABL & 2) != 0)
+    if constexpr (MF == 1)
+      compute16(smem + st_cur * STAGE);
+    else if constexpr ((ABL & 2) != 0)
       compute_pipe(smem + st_cur * STAGE);
     else
       compute(smem + st_cur * STAGE);
@@ -313,10 +463,14 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  x6_epilogue<BM, BN, WM, BN, TM, TN, NT, EPI, 1>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
+  if constexpr (MF == 1)
+    h3_epilogue16<BM, BN, WM, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wave, tid, ainv);
+  else
+    x6_epilogue<BM, BN, WM, BN, TM, TN, NT, EPI, 1>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
 }
 
-template <int BM, int BN, int WM, int EPI, int OCC, int BK, int NSTAGE, bool NMAJ = false, int ABL = 0>
+template <int BM, int BN, int WM, int EPI, int OCC, int BK, int NSTAGE, bool NMAJ = false, int ABL = 0,
+          int MF = 0>
 inline int launch_conv_h3_cfg(const ConvArgs& a, hipStream_t st) {
   if (!a.wh || !a.winv || a.Kpad % BK != 0 || (a.nseg == 2 && a.kseg1 % BK != 0) || a.N % BN != 0) {
     set_error("conv_h3: K/N not aligned to the tile or no split weights (Kpad=%d kseg1=%d N=%d)", a.Kpad,
@@ -333,10 +487,10 @@ inline int launch_conv_h3_cfg(const ConvArgs& a, hipStream_t st) {
     return SFA_E_INVALID;
   }
   if (a.nseg == 2)
-    hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 2, NMAJ, ABL>), dim3((unsigned)nblocks),
+    hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 2, NMAJ, ABL, MF>), dim3((unsigned)nblocks),
                        dim3((BM / WM) * 64), 0, st, a);
   else
-    hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 1, NMAJ, ABL>), dim3((unsigned)nblocks),
+    hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 1, NMAJ, ABL, MF>), dim3((unsigned)nblocks),
                        dim3((BM / WM) * 64), 0, st, a);
   SFA_LAUNCH_CHECK();
   return SFA_OK;

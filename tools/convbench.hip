@@ -167,6 +167,11 @@ struct Cand {
     "h3n " #BM "x" #BN " w" #WM " occ" #OCC " bk" #BK " st" #NS " nmaj" #NMAJ " abl" #ABL, BK, \
         [](const ConvArgs& a, hipStream_t s) { return launch_conv_h3_cfg<BM, BN, WM, EPI, OCC, BK, NS, NMAJ, ABL>(a, s); } \
   }
+#define CANDM(BM, BN, WM, EPI, OCC, NS, ABL)                                            \
+  Cand {                                                                                \
+    "h3m " #BM "x" #BN " w" #WM " occ" #OCC " bk32 st" #NS " abl" #ABL, 32,                 \
+        [](const ConvArgs& a, hipStream_t s) { return launch_conv_h3_cfg<BM, BN, WM, EPI, OCC, 32, NS, false, ABL, 1>(a, s); } \
+  }
 #define CANDA(BM, BN, WM, WN, BK, EPI, OCC, ABL) CANDG(BM, BN, WM, WN, BK, EPI, OCC, false, ABL)
 #define CAND(BM, BN, WM, WN, BK, EPI, OCC) CANDA(BM, BN, WM, WN, BK, EPI, OCC, 0)
 
@@ -189,7 +194,7 @@ int main(int argc, char** argv) {
       CANDH(256, 64, 32, EPI_STD, 1), CANDH(256, 64, 32, EPI_STD, 2), CANDH(128, 64, 32, EPI_STD, 2),
       CANDHK(256, 64, 32, EPI_STD, 1, 32, 3), CANDHK(128, 64, 32, EPI_STD, 2, 32, 2),
       CANDN(128, 64, 32, EPI_STD, 2, 32, 2, false, 0), CANDN(256, 64, 32, EPI_STD, 1, 16, 3, false, 0),
-      CANDN(128, 64, 32, EPI_STD, 2, 32, 2, false, 2), CANDN(256, 64, 32, EPI_STD, 1, 16, 3, false, 2),
+      CANDM(128, 64, 32, EPI_STD, 2, 2, 0), CANDM(128, 64, 32, EPI_STD, 2, 2, 2), CANDM(256, 64, 32, EPI_STD, 1, 2, 0),
   };
   std::vector<Cand> nbig = {
       CAND(64, 128, 32, 64, 16, EPI_STD, 4),
@@ -199,7 +204,8 @@ int main(int argc, char** argv) {
       CANDN(256, 128, 32, EPI_STD, 1, 16, 3, false, 0), CANDN(256, 128, 32, EPI_STD, 1, 32, 2, false, 0),
       CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 0), CANDN(128, 128, 32, EPI_STD, 1, 32, 3, false, 0),
       CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2), CANDN(128, 128, 32, EPI_STD, 1, 32, 3, false, 2),
-      CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 4), CANDN(256, 128, 32, EPI_STD, 1, 16, 3, false, 2),
+      CANDM(128, 128, 32, EPI_STD, 2, 2, 0), CANDM(128, 128, 32, EPI_STD, 2, 2, 2),
+      CANDM(128, 128, 32, EPI_STD, 1, 3, 0),
   };
   std::vector<Cand> heads = {
       CAND(128, 64, 32, 64, 16, EPI_HEAD, 4),
@@ -208,7 +214,8 @@ int main(int argc, char** argv) {
       CANDHK(256, 320, 32, EPI_HEAD, 1, 32, 2), CANDHK(128, 320, 32, EPI_HEAD, 1, 32, 2),
       CANDN(256, 320, 32, EPI_HEAD, 1, 32, 2, false, 0), CANDN(256, 320, 32, EPI_HEAD, 1, 16, 3, false, 0),
       CANDN(256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2), CANDN(256, 320, 32, EPI_HEAD, 1, 32, 2, false, 4),
-      CANDN(256, 320, 32, EPI_HEAD, 1, 32, 2, false, 6), CANDN(256, 320, 32, EPI_HEAD, 1, 16, 3, false, 2),
+      CANDN(256, 320, 32, EPI_HEAD, 1, 32, 2, false, 6), CANDM(256, 320, 32, EPI_HEAD, 1, 2, 0),
+      CANDM(256, 320, 32, EPI_HEAD, 1, 2, 2), CANDM(256, 320, 32, EPI_HEAD, 1, 2, 6),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
