@@ -305,7 +305,6 @@ def main():
             elapsed, threads = run_fusion(args, rank, world, dev), None
         else:
             elapsed, threads = run_stream(args, rank, world, dev)
-        elapsed, threads = run_stream(args, rank, world, dev)
         if world > 1:
             import torch.distributed as dist
             t = torch.tensor([elapsed], dtype=torch.float64,

@@ -156,6 +156,12 @@ struct ConvArgs {
   int hch[SFA_MAX_HEADS];
   int hoff[SFA_MAX_HEADS];
   float* hout;
+  // split-K (EPI_STD, fp16x3): workspace for [ksplit][M][N] partial sums, or null (no
+  // split); launch_conv picks ksplit for grids too small to fill the chip, the conv
+  // writes scaled partials and a reduce kernel applies the epilogue.
+  float* part;
+  size_t part_floats;
+  int ksplit;
 };
 
 int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t stream);

@@ -45,6 +45,18 @@ __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[
     for (int v = 0; v < 4; ++v) rinv[mi][v] = __shfl(ainv[mi], 4 * g + v, 64);
   if constexpr (EPI == EPI_STD) {
     AmaxRows am(a.OH * a.OW, m0);
+    float rv[TM][TN][4];  // residual tile loaded up front
+    if (a.res) {
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int m = min(m0 + wave * WM + mi * 16 + 4 * g + v, M - 1);
+            rv[mi][ni][v] = a.res[(size_t)m * a.N + n0 + ni * 16 + c16];
+          }
+    }
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
       const int n = n0 + ni * 16 + c16;
@@ -57,7 +69,7 @@ __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[
           const int m = m0 + wave * WM + mi * 16 + 4 * g + v;
           if (m < M) {
             float val = acc[mi][ni][v] * rinv[mi][v] * cs + bn;
-            if (a.res) val += a.res[(size_t)m * a.N + n];
+            if (a.res) val += rv[mi][ni][v];
             if (a.relu) val = fmaxf(val, 0.f);
             a.y[(size_t)m * a.N + n] = val;
             if (a.amax_out) am.add(a.amax_out, m, val);
@@ -157,10 +169,13 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n_tiles = a.N / BN;
-  const int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  const int m_tiles = (a.M + BM - 1) / BM;
+  const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
+  int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kz = lbid / (m_tiles * n_tiles);  // split-K slice of this block
+  lbid -= kz * (m_tiles * n_tiles);
   int mt, nt;
   if constexpr (NMAJ) {
-    const int m_tiles = (a.M + BM - 1) / BM;
     nt = lbid / m_tiles;
     mt = lbid - nt * m_tiles;
   } else {
@@ -432,10 +447,11 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
     }
   };
 
-  const int nk = a.Kpad / BK;
+  const int nk = a.Kpad / BK / nsplit;  // this block's K-tiles: kt0 .. kt0 + nk - 1
+  const int kt0 = kz * nk;
   // ring: tile kt lives in stage kt % NSTAGE; tiles kt+1 .. kt+NSTAGE-1 are in flight
 #pragma unroll
-  for (int p = 0; p < NSTAGE - 1; ++p) load_tile(p < nk ? p : nk - 1, smem + p * STAGE);
+  for (int p = 0; p < NSTAGE - 1; ++p) load_tile(kt0 + (p < nk ? p : nk - 1), smem + p * STAGE);
   if constexpr ((ABL & 4) != 0) {
     if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   }
@@ -450,7 +466,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
     __builtin_amdgcn_s_barrier();  // every wave's: stage kt complete; stage kt-1 no longer read
     if constexpr (!(ABL & 1)) {
       const int kn = kt + NSTAGE - 1;
-      load_tile(kn < nk ? kn : nk - 1, smem + st_next * STAGE);
+      load_tile(kt0 + (kn < nk ? kn : nk - 1), smem + st_next * STAGE);
     }
     if constexpr (MF == 1)
       compute16(smem + st_cur * STAGE);
@@ -462,11 +478,59 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
     st_next = st_next + 1 == NSTAGE ? 0 : st_next + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (nsplit > 1) {  // split-K: this slice's partial sums, scaled back (the reduce adds the rest)
+    float* part = a.part + (size_t)kz * M * a.N;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int v = 0; v < (MF ? 4 : 16); ++v) {
+          int row, col;
+          if constexpr (MF == 1) {
+            row = mi * 16 + 4 * (lane >> 4) + v;
+            col = ni * 16 + (lane & 15);
+          } else {
+            row = mi * 32 + (v & 3) + 8 * (v >> 2) + 4 * (lane >> 5);
+            col = ni * 32 + (lane & 31);
+          }
+          const float si = __shfl(ainv[mi], MF ? (row & 15) : (row & 31), 64);
+          const int m = m0 + wave * WM + row, n = n0 + col;
+          if (m < M) part[(size_t)m * a.N + n] = acc[mi][ni][v] * si * a.winv[n];
+        }
+    return;
+  }
   __syncthreads();
   if constexpr (MF == 1)
     h3_epilogue16<BM, BN, WM, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wave, tid, ainv);
   else
     x6_epilogue<BM, BN, WM, BN, TM, TN, NT, EPI, 1>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
+}
+
+// Split-K reduce: y = sum_z part[z] + bias (+ residual) (ReLU), per-frame max |y| — the
+// EPI_STD epilogue over float4 column groups; the slices are added in a fixed order.
+static __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArgs a) {
+  const int M = a.M, N = a.N;
+  const long long e0 = (long long)blockIdx.x * 1024;
+  const long long e = e0 + 4 * threadIdx.x;
+  AmaxRows am(a.OH * a.OW, (int)(e0 / N));
+  if (e < (long long)M * N) {
+    const int m = (int)(e / N), n = (int)(e - (long long)m * N);
+    x6_f32x4 s = *reinterpret_cast<const x6_f32x4*>(a.part + e);
+    for (int z = 1; z < a.ksplit; ++z) s += *reinterpret_cast<const x6_f32x4*>(a.part + (size_t)z * M * N + e);
+    s += *reinterpret_cast<const x6_f32x4*>(a.bias + n);
+    if (a.res) s += *reinterpret_cast<const x6_f32x4*>(a.res + e);
+    if (a.relu) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s[i] = fmaxf(s[i], 0.f);
+    }
+    *reinterpret_cast<x6_f32x4*>(a.y + e) = s;
+    if (a.amax_out) am.add(a.amax_out, m, fmaxf(fmaxf(fabsf(s[0]), fabsf(s[1])), fmaxf(fabsf(s[2]), fabsf(s[3]))));
+  }
+  if (a.amax_out) {
+    __shared__ float red[8];
+    amax_commit_block<4>(a.amax_out, am.fb0, am.mx0, am.mx1, red);
+  }
 }
 
 template <int BM, int BN, int WM, int EPI, int OCC, int BK, int NSTAGE, bool NMAJ = false, int ABL = 0,
@@ -481,7 +545,13 @@ inline int launch_conv_h3_cfg(const ConvArgs& a, hipStream_t st) {
     set_error("conv_h3: split weights >= 2 GiB");
     return SFA_E_UNSUPPORTED;
   }
-  const long long nblocks = (long long)ceil_div(a.M, BM) * (a.N / BN);
+  const int ks = a.ksplit > 1 ? a.ksplit : 1;
+  if (ks > 1 && (EPI != EPI_STD || (a.Kpad / BK) % ks != 0 || !a.part ||
+                 (size_t)ks * a.M * a.N > a.part_floats || a.N % 4 != 0)) {
+    set_error("conv_h3: split-K %d unsupported here (Kpad=%d N=%d)", ks, a.Kpad, a.N);
+    return SFA_E_UNSUPPORTED;
+  }
+  const long long nblocks = (long long)ceil_div(a.M, BM) * (a.N / BN) * ks;
   if (nblocks <= 0 || nblocks > 0x7fffffffll) {
     set_error("conv_h3: bad grid (M=%d N=%d)", a.M, a.N);
     return SFA_E_INVALID;
@@ -493,6 +563,11 @@ inline int launch_conv_h3_cfg(const ConvArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 1, NMAJ, ABL, MF>), dim3((unsigned)nblocks),
                        dim3((BM / WM) * 64), 0, st, a);
   SFA_LAUNCH_CHECK();
+  if (ks > 1) {
+    const long long nel = (long long)a.M * a.N;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((nel + 1023) / 1024)), dim3(256), 0, st, a);
+    SFA_LAUNCH_CHECK();
+  }
   return SFA_OK;
 }
 

@@ -57,11 +57,19 @@ def main():
     fwd = [r for r in rows if "kfpn_combine" in r["name"]]
     if fwd:
         nf = len(fwd)
-        conv = sum(r["dur"] for r in rows if re.search(r"conv_(mfma|x6g?)_kernel", r["name"]))
+        conv = sum(r["dur"] for r in rows if re.search(r"conv_(mfma|x6g?|h3)_kernel", r["name"]))
         aux = sum(r["dur"] for r in rows if re.search(r"maxpool|upsample|nchw3|kfpn", r["name"]))
         print(f"# forwards: {nf}; per forward: conv launches {conv / nf / 1e3:.1f} us, "
               f"maxpool/upsample/layout/kfpn {aux / nf / 1e3:.1f} us "
               f"(durations summed; concurrent launches overlap in wall time)")
+        # the dispatches of one forward in issue order (the one before the last kfpn_combine)
+        ends = [i for i, r in enumerate(rows) if "kfpn_combine" in r["name"]]
+        if len(ends) >= 2:
+            lo, hi = ends[-2] + 1, ends[-1] + 1
+            t0 = rows[lo]["start"]
+            print("\n# one forward in issue order (start offset us, duration us)")
+            for r in rows[lo:hi]:
+                print(f"{(r['start'] - t0) / 1e3:9.1f} {r['dur'] / 1e3:9.1f}  {short(r['name'])[:70]:70s} {r['grid']}")
     print("\n# per launch shape (grid = total work-items)")
     print(f"{'kernel':90s} {'grid':>22s} {'calls':>6s} {'avg_us':>10s}")
     for (k, g), d in sorted(by_shape.items(), key=lambda kv: -sum(kv[1])):
