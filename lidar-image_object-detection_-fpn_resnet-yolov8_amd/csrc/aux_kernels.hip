@@ -44,19 +44,16 @@ __global__ void __launch_bounds__(256) amax_nhwc4_kernel(const float4* __restric
   amax_commit_block<4>(amax, b, mx, 0.f, red);
 }
 
-// One thread per (output pixel, 4 channels).
+// One thread per (output pixel, 4 channels) of one output row; grid (ceil(OW * C4 / 256), OH,
+// B), 32-bit index math (C4 a power of two: no 64-bit divisions per thread).
 __global__ void __launch_bounds__(256) maxpool3s2_kernel(const float4* __restrict__ x,
-                                                         float4* __restrict__ y, int B, int H, int W,
-                                                         int C4, int OH, int OW) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)B * OH * OW * C4;
-  if (i >= total) return;
-  const int c = (int)(i % C4);
-  long long t = i / C4;
-  const int ox = (int)(t % OW);
-  t /= OW;
-  const int oy = (int)(t % OH);
-  const int b = (int)(t / OH);
+                                                         float4* __restrict__ y, int H, int W,
+                                                         int logC4, int OH, int OW) {
+  const int C4 = 1 << logC4;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= OW * C4) return;
+  const int c = idx & (C4 - 1), ox = idx >> logC4, oy = blockIdx.y, b = blockIdx.z;
+  const float4* xb = x + (size_t)b * H * W * C4;
   float4 m = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
 #pragma unroll
   for (int dy = 0; dy < 3; ++dy) {
@@ -66,65 +63,57 @@ __global__ void __launch_bounds__(256) maxpool3s2_kernel(const float4* __restric
     for (int dx = 0; dx < 3; ++dx) {
       const int ix = ox * 2 - 1 + dx;
       if ((unsigned)ix >= (unsigned)W) continue;
-      const float4 v = x[(((size_t)b * H + iy) * W + ix) * C4 + c];
+      const float4 v = xb[(iy * W + ix) * C4 + c];
       m.x = fmaxf(m.x, v.x);
       m.y = fmaxf(m.y, v.y);
       m.z = fmaxf(m.z, v.z);
       m.w = fmaxf(m.w, v.w);
     }
   }
-  y[i] = m;
+  y[(((size_t)b * OH + oy) * OW + ox) * C4 + c] = m;
 }
 
 // align_corners=True: src = dst * (in-1)/(out-1) in f32 (ATen area_pixel_compute_scale /
 // _source_index), i0 = floor(src), i1 = i0 + (i0 < in-1), l1 = src - i0, l0 = 1 - l1.
+// Grid (ceil(OW * C4 / 256), OH, B) as maxpool3s2_kernel.
 __global__ void __launch_bounds__(256) upsample2x_bilinear_kernel(const float4* __restrict__ x,
-                                                                  float4* __restrict__ y, int B,
-                                                                  int H, int W, int C4, float sh,
+                                                                  float4* __restrict__ y, int H,
+                                                                  int W, int logC4, float sh,
                                                                   float sw) {
-  const int OH = 2 * H, OW = 2 * W;
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)B * OH * OW * C4;
-  if (i >= total) return;
-  const int c = (int)(i % C4);
-  long long t = i / C4;
-  const int ox = (int)(t % OW);
-  t /= OW;
-  const int oy = (int)(t % OH);
-  const int b = (int)(t / OH);
+  const int C4 = 1 << logC4, OH = 2 * H, OW = 2 * W;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= OW * C4) return;
+  const int c = idx & (C4 - 1), ox = idx >> logC4, oy = blockIdx.y, b = blockIdx.z;
   const float fy = sh * (float)oy, fx = sw * (float)ox;
   const int y0 = (int)fy, x0 = (int)fx;
   const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
   const float ly1 = fy - (float)y0, lx1 = fx - (float)x0;
   const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
-  const size_t base = (size_t)b * H;
-  const float4 a00 = x[((base + y0) * W + x0) * C4 + c];
-  const float4 a01 = x[((base + y0) * W + x1) * C4 + c];
-  const float4 a10 = x[((base + y1) * W + x0) * C4 + c];
-  const float4 a11 = x[((base + y1) * W + x1) * C4 + c];
+  const float4* xb = x + (size_t)b * H * W * C4;
+  const float4 a00 = xb[(y0 * W + x0) * C4 + c];
+  const float4 a01 = xb[(y0 * W + x1) * C4 + c];
+  const float4 a10 = xb[(y1 * W + x0) * C4 + c];
+  const float4 a11 = xb[(y1 * W + x1) * C4 + c];
   float4 o;
   o.x = ly0 * (lx0 * a00.x + lx1 * a01.x) + ly1 * (lx0 * a10.x + lx1 * a11.x);
   o.y = ly0 * (lx0 * a00.y + lx1 * a01.y) + ly1 * (lx0 * a10.y + lx1 * a11.y);
   o.z = ly0 * (lx0 * a00.z + lx1 * a01.z) + ly1 * (lx0 * a10.z + lx1 * a11.z);
   o.w = ly0 * (lx0 * a00.w + lx1 * a01.w) + ly1 * (lx0 * a10.w + lx1 * a11.w);
-  y[i] = o;
+  y[(((size_t)b * OH + oy) * OW + ox) * C4 + c] = o;
 }
 
 // Planar level buffers: Lk[ch][b][y][x] (ch over all heads, forward order).
 // Level 0 is at (h/2, w/2) and resized by nearest (src = dst // 2, F.interpolate
 // default mode with an exact 0.5 scale).
+// grid (ceil(h * w / 256), B, channels): 32-bit index math.
 __global__ void __launch_bounds__(256) kfpn_combine_kernel(const float* __restrict__ L0,
                                                            const float* __restrict__ L1,
                                                            const float* __restrict__ L2,
                                                            KfpnOut o, int B, int h, int w) {
   const int hw = h * w;
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long total = (long long)o.total_ch * B * hw;
-  if (i >= total) return;
-  const int ch = (int)(i / ((long long)B * hw));
-  const int rem = (int)(i - (long long)ch * B * hw);
-  const int b = rem / hw;
-  const int p = rem - b * hw;
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= hw) return;
+  const int b = blockIdx.y, ch = blockIdx.z;
   const int yy = p / w, xx = p - yy * w;
   const int h0 = h / 2, w0 = w / 2;
   const float v0 = L0[((size_t)ch * B + b) * (h0 * w0) + (yy >> 1) * w0 + (xx >> 1)];
@@ -194,12 +183,23 @@ int launch_amax_nhwc4(const float* x, int B, int H, int W, unsigned* amax, hipSt
   return SFA_OK;
 }
 
+static int pow2_c4(int C, const char* what) {
+  const int C4 = C / 4;
+  if ((C & 3) || C4 <= 0 || (C4 & (C4 - 1))) {
+    set_error("%s: channels %d must be 4 x a power of two", what, C);
+    return -1;
+  }
+  return ilog2(C4);
+}
+
 int launch_maxpool3s2(const float* x, float* y, int B, int H, int W, int C, hipStream_t st) {
   const int OH = (H + 2 - 3) / 2 + 1, OW = (W + 2 - 3) / 2 + 1;
-  const long long n = (long long)B * OH * OW * (C / 4);
-  hipLaunchKernelGGL(maxpool3s2_kernel, dim3(grid_of(n)), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), B, H, W, C / 4,
-                     OH, OW);
+  const int lc = pow2_c4(C, "maxpool3s2");
+  if (lc < 0) return SFA_E_UNSUPPORTED;
+  SFA_CHECK_ARG(B <= 65535 && OH <= 65535, "maxpool3s2: grid too large");
+  hipLaunchKernelGGL(maxpool3s2_kernel, dim3((unsigned)((OW * (C / 4) + 255) / 256), (unsigned)OH, (unsigned)B),
+                     dim3(256), 0, st, reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), H, W,
+                     lc, OH, OW);
   SFA_LAUNCH_CHECK();
   return SFA_OK;
 }
@@ -207,18 +207,21 @@ int launch_maxpool3s2(const float* x, float* y, int B, int H, int W, int C, hipS
 int launch_upsample2x(const float* x, float* y, int B, int H, int W, int C, hipStream_t st) {
   const float sh = H > 1 ? (float)(H - 1) / (float)(2 * H - 1) : 0.f;
   const float sw = W > 1 ? (float)(W - 1) / (float)(2 * W - 1) : 0.f;
-  const long long n = (long long)B * 4 * H * W * (C / 4);
-  hipLaunchKernelGGL(upsample2x_bilinear_kernel, dim3(grid_of(n)), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), B, H, W, C / 4,
-                     sh, sw);
+  const int lc = pow2_c4(C, "upsample2x");
+  if (lc < 0) return SFA_E_UNSUPPORTED;
+  SFA_CHECK_ARG(B <= 65535 && 2 * H <= 65535, "upsample2x: grid too large");
+  hipLaunchKernelGGL(upsample2x_bilinear_kernel,
+                     dim3((unsigned)((2 * W * (C / 4) + 255) / 256), (unsigned)(2 * H), (unsigned)B), dim3(256), 0,
+                     st, reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), H, W, lc, sh, sw);
   SFA_LAUNCH_CHECK();
   return SFA_OK;
 }
 
 int launch_kfpn(const float* L0, const float* L1, const float* L2, const KfpnOut& o, int B, int h,
                 int w, hipStream_t st) {
-  const long long n = (long long)o.total_ch * B * h * w;
-  hipLaunchKernelGGL(kfpn_combine_kernel, dim3(grid_of(n)), dim3(256), 0, st, L0, L1, L2, o, B, h, w);
+  SFA_CHECK_ARG(B <= 65535 && o.total_ch <= 65535, "kfpn: grid too large");
+  hipLaunchKernelGGL(kfpn_combine_kernel, dim3((unsigned)((h * w + 255) / 256), (unsigned)B, (unsigned)o.total_ch),
+                     dim3(256), 0, st, L0, L1, L2, o, B, h, w);
   SFA_LAUNCH_CHECK();
   return SFA_OK;
 }

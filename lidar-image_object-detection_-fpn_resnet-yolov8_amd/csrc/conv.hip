@@ -3,6 +3,7 @@
 #include "conv_kernel.h"
 #include "conv_x6_kernel.h"
 #include "conv_h3_kernel.h"
+#include "conv_h3s_kernel.h"
 
 namespace sfa {
 
@@ -29,15 +30,28 @@ static int launch_conv_x6(const ConvArgs& a, int epilogue, hipStream_t st) {
   return rc;
 }
 
-// fp16x3 tiles per shape (tools/convbench.hip sweeps, profiles/r01_convbench_h3n*.txt,
-// r01_convbench_h3m.txt): the streamlined conv_h3_kernel (fixed DMA slots per wave, pipelined
-// fragment reads) with BK = 32 and a 2-deep ring wherever K allows it; 16x16x32 MFMAs for the
-// heads and the 64-wide layers (-1.5 % / -11 %), 32x32x16 for the 128..512-wide ones; the 7x7
-// stem (K = 196) on BK 16; conv_x6g_kernel<..., PREC 1> tiles as the fallback.
+// One-segment 3x3 / stride 1 / pad 1 conv with 32-channel chunks: conv_h3s_kernel applies.
+static bool strip_ok(const ConvArgs& a) {
+  const ConvSeg& g = a.seg[0];
+  return a.nseg == 1 && g.KH == 3 && g.KW == 3 && g.stride == 1 && g.pad == 1 && g.C >= 32 &&
+         (g.C & 31) == 0 && a.Kpad == 9 * g.C && a.OH == g.H && a.OW == g.W;
+}
+
+// fp16x3 tiles per shape (tools/convbench.hip sweeps: profiles/r01_convbench_h3n*.txt,
+// r01_convbench_h3m.txt, r01_convbench_strip_splitk.txt):
+//  * heads: conv_h3_kernel on 16x16x32 MFMAs, 256x320 (all 5 heads of a level per tile);
+//  * 3x3/s1 body convs: conv_h3s_kernel (A staged once per kh as a row strip for the three kw
+//    taps), 128-row tiles at 2 blocks/CU: -4..5 % vs per-tap staging;
+//  * the rest (stride-2 convs, 2-segment convs, 1x1 FPN convs, the stem): conv_h3_kernel,
+//    16x16x32 for the 64-wide ones, 32x32x16 for the 128..512-wide ones, BK 16 for the stem;
+//  * split-K 2 for the 512-wide (layer4) convs, whose 184 tiles cannot fill 256 CUs (-13..16 %);
+//    picked from the width only, so a frame's arithmetic never depends on the batch.
+// conv_x6g_kernel<..., PREC 1> tiles as the fallback.
 static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;
   auto ok = [](int rc) { return rc != SFA_E_UNSUPPORTED; };
   int rc = SFA_E_UNSUPPORTED;
+  const bool strip = strip_ok(a);
   if (epilogue == EPI_HEAD) {
     if (a.N == 320) {
       rc = launch_conv_h3_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2, 1>(a, st);
@@ -47,14 +61,23 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     return rc;
   }
   if (a.N == 64) {
-    if (a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
+    if (strip) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 2>(a, st);
+    if (!ok(rc) && a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
     if (!ok(rc)) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 16, 3, false, 0>(a, st);
     if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_STD, 1, 16, 3, 0, 64, 1>(a, st);
     return rc;
   }
   if (a.N % 128 == 0) {
-    rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(a, st);
-    if (!ok(rc)) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2, 16, 3, 0, 128, 1>(a, st);
+    ConvArgs b = a;
+    b.ksplit = a.part && a.N >= 512 ? 2 : 1;
+    if (strip) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
+    if (!ok(rc)) rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
+    if (!ok(rc) && b.ksplit > 1) {  // K not divisible into the slices: no split
+      b.ksplit = 1;
+      if (strip) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
+      if (!ok(rc)) rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
+    }
+    if (!ok(rc)) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2, 16, 3, 0, 128, 1>(b, st);
   }
   return rc;
 }

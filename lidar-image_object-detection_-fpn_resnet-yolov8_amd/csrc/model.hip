@@ -461,7 +461,8 @@ namespace sfa {
 
 // Activation buffers of one forward (NHWC f32), carved from the workspace.
 struct Bufs {
-  size_t xin, s0, p0, t[4], a[4], l[4], up1, c1, up2, c2, up3, up4, L0, L1, L2, amax, total;
+  size_t xin, s0, p0, t[4], a[4], l[4], up1, c1, up2, c2, up3, up4, L0, L1, L2, amax, part, part_floats,
+      total;
 };
 
 // fp16x3 activation maxima (conv.h): per tensor a conv reads (named by its producer), B
@@ -502,6 +503,9 @@ static Bufs plan_bufs(const sfa_arch* arch, int B, int H, int W) {
   b.L1 = take((size_t)nch * B * P4);
   b.L2 = take((size_t)nch * B * P4);
   b.amax = take((size_t)AM_COUNT * B * SFA_AMAX_WORDS);
+  // split-K partial sums of the widest convs (conv.hip: 2 slices at 512 channels; room for 4)
+  b.part_floats = (size_t)4 * B * (H / 32) * (W / 32) * 512;
+  b.part = take(b.part_floats);
   b.total = cur;
   return b;
 }
@@ -598,6 +602,8 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.amax_in[0] = in0 >= 0 ? AM(in0) : nullptr;
     a.amax_in[1] = in1 >= 0 ? AM(in1) : nullptr;
     a.amax_out = out >= 0 ? AM(out) : nullptr;
+    a.part = F(bf.part);
+    a.part_floats = bf.part_floats;
   };
 
   const float* xin = x;

@@ -16,6 +16,7 @@
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_x6_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3_kernel.h"
+#include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3s_kernel.h"
 
 namespace sfa {
 void set_error(const char* fmt, ...) {
@@ -172,6 +173,30 @@ struct Cand {
     "h3m " #BM "x" #BN " w" #WM " occ" #OCC " bk32 st" #NS " abl" #ABL, 32,                 \
         [](const ConvArgs& a, hipStream_t s) { return launch_conv_h3_cfg<BM, BN, WM, EPI, OCC, 32, NS, false, ABL, 1>(a, s); } \
   }
+static float* g_part = nullptr;
+static const size_t g_part_floats = 64u << 20;
+#define CANDK(BM, BN, WM, EPI, OCC, NS, ABL, MF, KS)                                                \
+  Cand {                                                                                          \
+    "h3k " #BM "x" #BN " w" #WM " occ" #OCC " st" #NS " abl" #ABL " mf" #MF " ks" #KS, 32,           \
+        [](const ConvArgs& a, hipStream_t s) {                                                    \
+          ConvArgs b = a;                                                                         \
+          b.ksplit = KS;                                                                          \
+          b.part = g_part;                                                                        \
+          b.part_floats = g_part_floats;                                                          \
+          return launch_conv_h3_cfg<BM, BN, WM, EPI, OCC, 32, NS, false, ABL, MF>(b, s);          \
+        }                                                                                         \
+  }
+#define CANDT(BM, BN, WM, EPI, OCC, KS)                                                            \
+  Cand {                                                                                          \
+    "h3strip " #BM "x" #BN " w" #WM " occ" #OCC " ks" #KS, 32,                                      \
+        [](const ConvArgs& a, hipStream_t s) {                                                    \
+          ConvArgs b = a;                                                                         \
+          b.ksplit = KS;                                                                          \
+          b.part = g_part;                                                                        \
+          b.part_floats = g_part_floats;                                                          \
+          return launch_conv_h3s_cfg<BM, BN, WM, EPI, OCC>(b, s);                                 \
+        }                                                                                         \
+  }
 #define CANDA(BM, BN, WM, WN, BK, EPI, OCC, ABL) CANDG(BM, BN, WM, WN, BK, EPI, OCC, false, ABL)
 #define CAND(BM, BN, WM, WN, BK, EPI, OCC) CANDA(BM, BN, WM, WN, BK, EPI, OCC, 0)
 
@@ -190,35 +215,25 @@ int main(int argc, char** argv) {
   };
   std::vector<Cand> n64 = {
       CAND(128, 64, 32, 64, 16, EPI_STD, 4),
-      CANDXG(256, 64, 32, EPI_STD, 1),
-      CANDH(256, 64, 32, EPI_STD, 1), CANDH(256, 64, 32, EPI_STD, 2), CANDH(128, 64, 32, EPI_STD, 2),
-      CANDHK(256, 64, 32, EPI_STD, 1, 32, 3), CANDHK(128, 64, 32, EPI_STD, 2, 32, 2),
-      CANDN(128, 64, 32, EPI_STD, 2, 32, 2, false, 0), CANDN(256, 64, 32, EPI_STD, 1, 16, 3, false, 0),
-      CANDM(128, 64, 32, EPI_STD, 2, 2, 0), CANDM(128, 64, 32, EPI_STD, 2, 2, 2), CANDM(256, 64, 32, EPI_STD, 1, 2, 0),
+      CANDM(256, 64, 32, EPI_STD, 1, 2, 0), CANDM(256, 64, 32, EPI_STD, 1, 2, 1),
+      CANDT(256, 64, 32, EPI_STD, 1, 1), CANDT(128, 64, 32, EPI_STD, 2, 1),
   };
   std::vector<Cand> nbig = {
       CAND(64, 128, 32, 64, 16, EPI_STD, 4),
-      CANDX(128, 128, 64, 64, 16, EPI_STD, 2), CANDXG(128, 128, 32, EPI_STD, 2), CANDX(64, 128, 32, 64, 32, EPI_STD, 2),
-      CANDH(128, 128, 32, EPI_STD, 2), CANDH(256, 128, 32, EPI_STD, 1), CANDH(64, 128, 32, EPI_STD, 2),
-      CANDHK(128, 128, 32, EPI_STD, 2, 32, 2), CANDHK(128, 128, 32, EPI_STD, 1, 32, 3),
-      CANDN(256, 128, 32, EPI_STD, 1, 16, 3, false, 0), CANDN(256, 128, 32, EPI_STD, 1, 32, 2, false, 0),
-      CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 0), CANDN(128, 128, 32, EPI_STD, 1, 32, 3, false, 0),
-      CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2), CANDN(128, 128, 32, EPI_STD, 1, 32, 3, false, 2),
-      CANDM(128, 128, 32, EPI_STD, 2, 2, 0), CANDM(128, 128, 32, EPI_STD, 2, 2, 2),
-      CANDM(128, 128, 32, EPI_STD, 1, 3, 0),
+      CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2), CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 3),
+      CANDK(128, 128, 32, EPI_STD, 2, 2, 2, 0, 2), CANDK(128, 128, 32, EPI_STD, 2, 2, 2, 0, 4),
+      CANDK(128, 128, 32, EPI_STD, 2, 2, 2, 0, 8),
+      CANDT(128, 128, 32, EPI_STD, 2, 1), CANDT(256, 128, 32, EPI_STD, 1, 1),
+      CANDT(128, 128, 32, EPI_STD, 2, 2), CANDT(128, 128, 32, EPI_STD, 2, 4),
   };
   std::vector<Cand> heads = {
       CAND(128, 64, 32, 64, 16, EPI_HEAD, 4),
-      CANDXG(256, 320, 32, EPI_HEAD, 1),
-      CANDH(256, 320, 32, EPI_HEAD, 1), CANDH(128, 320, 32, EPI_HEAD, 1),
-      CANDHK(256, 320, 32, EPI_HEAD, 1, 32, 2), CANDHK(128, 320, 32, EPI_HEAD, 1, 32, 2),
-      CANDN(256, 320, 32, EPI_HEAD, 1, 32, 2, false, 0), CANDN(256, 320, 32, EPI_HEAD, 1, 16, 3, false, 0),
-      CANDN(256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2), CANDN(256, 320, 32, EPI_HEAD, 1, 32, 2, false, 4),
-      CANDN(256, 320, 32, EPI_HEAD, 1, 32, 2, false, 6), CANDM(256, 320, 32, EPI_HEAD, 1, 2, 0),
-      CANDM(256, 320, 32, EPI_HEAD, 1, 2, 2), CANDM(256, 320, 32, EPI_HEAD, 1, 2, 6),
+      CANDM(256, 320, 32, EPI_HEAD, 1, 2, 2), CANDM(256, 320, 32, EPI_HEAD, 1, 2, 3),
+      CANDT(256, 320, 32, EPI_HEAD, 1, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
+  CK(hipMalloc(&g_part, g_part_floats * 4));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
