@@ -63,7 +63,7 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (a.N == 64) {
     if (strip) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 2>(a, st);
     if (!ok(rc) && a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
-    if (!ok(rc)) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 16, 3, false, 0>(a, st);
+    if (!ok(rc)) rc = launch_conv_h3_cfg<128, 64, 32, EPI_STD, 2, 16, 3, false, 0>(a, st);
     if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_STD, 1, 16, 3, 0, 64, 1>(a, st);
     return rc;
   }

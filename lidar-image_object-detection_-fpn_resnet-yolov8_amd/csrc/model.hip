@@ -284,7 +284,7 @@ struct sfa_model {
   // of the FPN and the level-1/2 heads); created with the model on the current device,
   // used only when the forward's stream is on that device.
   hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, mid = nullptr;
   int device = -1;
   std::mutex fork_mu;  // fork ... join of one forward is not interleaved with another's
 };
@@ -430,7 +430,8 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   if (hipGetDevice(&m->device) != hipSuccess ||
       hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&m->fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&m->join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&m->join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&m->mid, hipEventDisableTiming) != hipSuccess) {
     // no device (or no stream): the forward runs every launch on the caller's stream
     (void)hipGetLastError();
     m->side = nullptr;
@@ -443,6 +444,7 @@ extern "C" void sfa_model_destroy(sfa_model* model) {
   if (!model) return;
   if (model->fork) (void)hipEventDestroy(model->fork);
   if (model->join) (void)hipEventDestroy(model->join);
+  if (model->mid) (void)hipEventDestroy(model->mid);
   if (model->side) (void)hipStreamDestroy(model->side);
   delete model;
 }
@@ -733,7 +735,6 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     SFA_HIP_TRY(hipEventRecord(m->fork, st));
     SFA_HIP_TRY(hipStreamWaitEvent(m->side, m->fork, 0));
     SFA_RC(launch_head(0, m->side));
-    SFA_HIP_TRY(hipEventRecord(m->join, m->side));
   } else {
     SFA_RC(launch_head(0, st));
   }
@@ -756,8 +757,17 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     io(a, AM_FPN + 1, blk_slot(0, 1, 1), AM_FPN + 2);
     SFA_RC(launch_conv(a, EPI_STD, m->math, st));
   }
+  // level 2 (needs up_level4, just written) on the side stream after level 0, level 1 here:
+  // the two 1,444-tile launches run side by side, so neither one's last partial wave of tiles
+  // leaves CUs idle
+  if (overlap) {
+    SFA_HIP_TRY(hipEventRecord(m->mid, st));
+    SFA_HIP_TRY(hipStreamWaitEvent(m->side, m->mid, 0));
+    SFA_RC(launch_head(2, m->side));
+    SFA_HIP_TRY(hipEventRecord(m->join, m->side));
+  }
   SFA_RC(launch_head(1, st));
-  SFA_RC(launch_head(2, st));
+  if (!overlap) SFA_RC(launch_head(2, st));
   if (overlap) SFA_HIP_TRY(hipStreamWaitEvent(st, m->join, 0));
   // apply_kfpn (fpn_resnet.py:248-254)
   KfpnOut ko;

@@ -216,6 +216,8 @@ int main(int argc, char** argv) {
   std::vector<Cand> n64 = {
       CAND(128, 64, 32, 64, 16, EPI_STD, 4),
       CANDM(256, 64, 32, EPI_STD, 1, 2, 0), CANDM(256, 64, 32, EPI_STD, 1, 2, 1),
+      CANDN(256, 64, 32, EPI_STD, 1, 16, 3, false, 0), CANDN(256, 64, 32, EPI_STD, 1, 16, 3, false, 2),
+      CANDM(256, 64, 32, EPI_STD, 1, 3, 0), CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
       CANDT(256, 64, 32, EPI_STD, 1, 1), CANDT(128, 64, 32, EPI_STD, 2, 1),
   };
   std::vector<Cand> nbig = {

@@ -4,8 +4,5 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
 tail -2 gpurun_out/t_gpu.txt
 timeout -k 10 300 python bench.py > gpurun_out/b_main.json 2> gpurun_out/b_main.err || { echo "bench failed"; tail gpurun_out/b_main.err; exit 1; }
 cat gpurun_out/b_main.json
-rm -rf gpurun_out/prof_cur
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_cur -o run --output-format csv -- python bench.py --inflight 1 --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/b_prof.json 2> gpurun_out/b_prof.err || { echo "rocprof failed"; tail gpurun_out/b_prof.err; exit 1; }
-f=$(find gpurun_out/prof_cur -name "*kernel_trace.csv" | head -1)
-python3 tools/rocprof_summary.py "$f" > gpurun_out/prof_cur_summary.txt
-head -70 gpurun_out/prof_cur_summary.txt
+timeout -k 10 300 python bench.py --inflight 3 --no-cpu-baseline > gpurun_out/b_if3.json 2> gpurun_out/b_if3.err || { echo "bench3 failed"; tail gpurun_out/b_if3.err; exit 1; }
+cut -c1-200 gpurun_out/b_if3.json
