@@ -76,6 +76,22 @@ __global__ void __launch_bounds__(256) maxpool3s2_kernel(const float4* __restric
 // align_corners=True: src = dst * (in-1)/(out-1) in f32 (ATen area_pixel_compute_scale /
 // _source_index), i0 = floor(src), i1 = i0 + (i0 < in-1), l1 = src - i0, l0 = 1 - l1.
 // Grid (ceil(OW * C4 / 256), OH, B) as maxpool3s2_kernel.
+__device__ __forceinline__ float4 bilerp4(float ly0, float ly1, float lx0, float lx1, const float4& a00,
+                                          const float4& a01, const float4& a10, const float4& a11) {
+  float4 o;
+  o.x = ly0 * (lx0 * a00.x + lx1 * a01.x) + ly1 * (lx0 * a10.x + lx1 * a11.x);
+  o.y = ly0 * (lx0 * a00.y + lx1 * a01.y) + ly1 * (lx0 * a10.y + lx1 * a11.y);
+  o.z = ly0 * (lx0 * a00.z + lx1 * a01.z) + ly1 * (lx0 * a10.z + lx1 * a11.z);
+  o.w = ly0 * (lx0 * a00.w + lx1 * a01.w) + ly1 * (lx0 * a10.w + lx1 * a11.w);
+  return o;
+}
+
+// Each thread owns one (output column, channel quad) over UP_ROWS consecutive output
+// rows: with align_corners the source row advances by at most one per output row, so
+// the two source rows stay in registers and are reloaded only when y0 moves (about
+// 1.5 float4 loads per output instead of 4). Output rows are written in full 16-B quads
+// along (ox, c): coalesced.
+constexpr int UP_ROWS = 4;
 __global__ void __launch_bounds__(256) upsample2x_bilinear_kernel(const float4* __restrict__ x,
                                                                   float4* __restrict__ y, int H,
                                                                   int W, int logC4, float sh,
@@ -83,23 +99,42 @@ __global__ void __launch_bounds__(256) upsample2x_bilinear_kernel(const float4* 
   const int C4 = 1 << logC4, OH = 2 * H, OW = 2 * W;
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= OW * C4) return;
-  const int c = idx & (C4 - 1), ox = idx >> logC4, oy = blockIdx.y, b = blockIdx.z;
-  const float fy = sh * (float)oy, fx = sw * (float)ox;
-  const int y0 = (int)fy, x0 = (int)fx;
-  const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
-  const float ly1 = fy - (float)y0, lx1 = fx - (float)x0;
-  const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+  const int c = idx & (C4 - 1), ox = idx >> logC4, b = blockIdx.z;
+  const int oy0 = blockIdx.y * UP_ROWS;
+  const float fx = sw * (float)ox;
+  const int x0 = (int)fx;
+  const int x1 = x0 + (x0 < W - 1 ? 1 : 0);
+  const float lx1 = fx - (float)x0, lx0 = 1.f - lx1;
   const float4* xb = x + (size_t)b * H * W * C4;
-  const float4 a00 = xb[(y0 * W + x0) * C4 + c];
-  const float4 a01 = xb[(y0 * W + x1) * C4 + c];
-  const float4 a10 = xb[(y1 * W + x0) * C4 + c];
-  const float4 a11 = xb[(y1 * W + x1) * C4 + c];
-  float4 o;
-  o.x = ly0 * (lx0 * a00.x + lx1 * a01.x) + ly1 * (lx0 * a10.x + lx1 * a11.x);
-  o.y = ly0 * (lx0 * a00.y + lx1 * a01.y) + ly1 * (lx0 * a10.y + lx1 * a11.y);
-  o.z = ly0 * (lx0 * a00.z + lx1 * a01.z) + ly1 * (lx0 * a10.z + lx1 * a11.z);
-  o.w = ly0 * (lx0 * a00.w + lx1 * a01.w) + ly1 * (lx0 * a10.w + lx1 * a11.w);
-  y[(((size_t)b * OH + oy) * OW + ox) * C4 + c] = o;
+  const int o0 = x0 * C4 + c, o1 = x1 * C4 + c, rs = W * C4;
+  int cy0 = -1, cy1 = -1;
+  float4 a00, a01, a10, a11;
+  float4* yb = y + ((size_t)b * OH * OW + (size_t)oy0 * OW + ox) * C4 + c;
+#pragma unroll
+  for (int r = 0; r < UP_ROWS; ++r) {
+    const int oy = oy0 + r;
+    if (oy >= OH) break;
+    const float fy = sh * (float)oy;
+    const int y0 = (int)fy;
+    const int y1 = y0 + (y0 < H - 1 ? 1 : 0);
+    if (y0 != cy0) {
+      if (y0 == cy1) {
+        a00 = a10;
+        a01 = a11;
+      } else {
+        a00 = xb[y0 * rs + o0];
+        a01 = xb[y0 * rs + o1];
+      }
+      cy0 = y0;
+    }
+    if (y1 != cy1) {
+      a10 = xb[y1 * rs + o0];
+      a11 = xb[y1 * rs + o1];
+      cy1 = y1;
+    }
+    const float ly1 = fy - (float)y0, ly0 = 1.f - ly1;
+    yb[(size_t)r * OW * C4] = bilerp4(ly0, ly1, lx0, lx1, a00, a01, a10, a11);
+  }
 }
 
 // Planar level buffers: Lk[ch][b][y][x] (ch over all heads, forward order).
@@ -211,7 +246,8 @@ int launch_upsample2x(const float* x, float* y, int B, int H, int W, int C, hipS
   if (lc < 0) return SFA_E_UNSUPPORTED;
   SFA_CHECK_ARG(B <= 65535 && 2 * H <= 65535, "upsample2x: grid too large");
   hipLaunchKernelGGL(upsample2x_bilinear_kernel,
-                     dim3((unsigned)((2 * W * (C / 4) + 255) / 256), (unsigned)(2 * H), (unsigned)B), dim3(256), 0,
+                     dim3((unsigned)((2 * W * (C / 4) + 255) / 256), (unsigned)((2 * H + UP_ROWS - 1) / UP_ROWS), (unsigned)B),
+                     dim3(256), 0,
                      st, reinterpret_cast<const float4*>(x), reinterpret_cast<float4*>(y), H, W, lc, sh, sw);
   SFA_LAUNCH_CHECK();
   return SFA_OK;

@@ -45,7 +45,9 @@ inline bool make_seg(ConvSeg& g, const float* x, int B, int H, int W, int C, int
   return bytes < (1ull << 31);
 }
 
-enum ConvEpilogue { EPI_STD = 0, EPI_HEAD = 1 };
+// EPI_POOL (fp16x3 stem): bias + ReLU, then the 3x3/s2/p1 max-pool of the tile in LDS;
+// y is the POOLED output (zeroed beforehand), rows of a block = one 16x16 spatial tile.
+enum ConvEpilogue { EPI_STD = 0, EPI_HEAD = 1, EPI_POOL = 2 };
 
 // fp16x3 activation scales (SFA_MATH_FP16X3).  max |x| of an activation tensor is kept
 // PER FRAME (so a frame's result never depends on the rest of its batch), each in

@@ -107,6 +107,14 @@ int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t st) {
     set_error("conv: bad kseg1 %d", a.kseg1);
     return SFA_E_UNSUPPORTED;
   }
+  if (epilogue == EPI_POOL) {  // fused stem + max-pool: fp16x3 only; the caller falls back
+    if (math != SFA_MATH_FP16X3 || !a.wh || !a.winv || a.nseg != 1 || a.N != 64 || !a.relu || a.res ||
+        a.ksplit > 1 || a.OH % 8 != 0 || a.OW % 16 != 0) {
+      set_error("conv: fused max-pool epilogue unsupported here (OH=%d OW=%d N=%d)", a.OH, a.OW, a.N);
+      return SFA_E_UNSUPPORTED;
+    }
+    return launch_conv_h3_cfg<128, 64, 32, EPI_POOL, 2, 16, 3, false, 0, 0>(a, st);  // the stem's tile
+  }
   if (math == SFA_MATH_FP16X3) {
     const int rc = launch_conv_h3(a, epilogue, st);
     if (rc != SFA_E_UNSUPPORTED) return rc;

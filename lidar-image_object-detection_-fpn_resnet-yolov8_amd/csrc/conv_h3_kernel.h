@@ -126,6 +126,77 @@ __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[
   }
 }
 
+// Stem + max-pool (fpn_resnet.py:179-182: conv1 -> bn1 -> relu -> maxpool 3x3/s2/p1) for
+// the 32x32x16 form. The block's BM rows are one TRH x 16 tile (th, tw) of frame b of the
+// conv output (TRH = BM / 16); ReLU(conv + b) goes to LDS, then the block writes the pooled
+// cells whose window touches the tile: pooled rows TR th .. TR th + TR (TR = TRH / 2),
+// columns 8 tw .. 8 tw + 8 (window rows 2 py - 1 .. 2 py + 1 cut to the tile). Cells whose
+// window lies wholly inside the tile (j in 1..TR-1, i in 1..7) have one writer and are
+// stored; the border cells are shared with the up/left neighbours and combined with
+// atomicMax on the f32 bits, exact because the values are >= +0 (ReLU, canonical +0) and
+// the pooled buffer is zeroed first. The pooled max is the conv output's max, recorded per
+// frame as the stem's amax (maxpool keeps it).
+template <int BM, int BN, int WM, int TM, int TN, int NT>
+__device__ __forceinline__ void h3_pool_epilogue(const ConvArgs& a, x6_f32x16 (&acc)[TM][TN],
+                                                 unsigned char* smem, int m0, int wave, int tid,
+                                                 const float (&ainv)[TM]) {
+  constexpr int LD = BN + 4;  // float4-aligned rows
+  float* T = reinterpret_cast<float*>(smem);
+  const int lane = tid & 63, r = lane & 31, h = lane >> 5;
+  float mx = 0.f;
+#pragma unroll
+  for (int ni = 0; ni < TN; ++ni) {
+    const int n = ni * 32 + r;
+    const float bn = a.bias[n];
+    const float cs = a.winv[n];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) {
+        const int row = wave * WM + mi * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+        const float rinv = __shfl(ainv[mi], (v & 3) + 8 * (v >> 2) + 4 * h, 64);
+        float val = acc[mi][ni][v] * rinv * cs + bn;
+        val = val > 0.f ? val : 0.f;
+        T[row * LD + n] = val;
+        mx = fmaxf(mx, val);
+      }
+  }
+  const int P = a.OH * a.OW;
+  const int b = m0 / P;
+  if (a.amax_out)
+    amax_commit_block<NT / 64>(a.amax_out, b, mx, 0.f, T + BM * LD);  // includes __syncthreads
+  else
+    __syncthreads();
+  constexpr int TRH = BM / 16, TR = TRH / 2;  // conv rows / pooled rows per tile
+  const int tile = (m0 - b * P) / BM, tw_n = a.OW >> 4;
+  const int th = tile / tw_n, tw = tile - th * tw_n;
+  const int PH = a.OH >> 1, PW = a.OW >> 1;
+  constexpr int C4 = BN / 4;
+  for (int idx = tid; idx < (TR + 1) * 9 * C4; idx += NT) {
+    const int c4 = idx % C4, cell = idx / C4;
+    const int j = cell / 9, i = cell - 9 * (cell / 9);
+    const int py = TR * th + j, px = 8 * tw + i;
+    if (py >= PH || px >= PW) continue;
+    const int r0 = 2 * j - 1 > 0 ? 2 * j - 1 : 0, r1 = 2 * j + 1 < TRH - 1 ? 2 * j + 1 : TRH - 1;
+    const int q0 = 2 * i - 1 > 0 ? 2 * i - 1 : 0, q1 = 2 * i + 1 < 15 ? 2 * i + 1 : 15;
+    x6_f32x4 m = {0.f, 0.f, 0.f, 0.f};
+    for (int rr = r0; rr <= r1; ++rr)
+      for (int qq = q0; qq <= q1; ++qq) {
+        const x6_f32x4 t = *reinterpret_cast<const x6_f32x4*>(T + (rr * 16 + qq) * LD + 4 * c4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], t[e]);
+      }
+    float* dst = a.y + ((size_t)(b * PH + py) * PW + px) * BN + 4 * c4;
+    if (j >= 1 && j < TR && i >= 1 && i <= 7) {
+      *reinterpret_cast<x6_f32x4*>(dst) = m;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (m[e] > 0.f) atomicMax(reinterpret_cast<unsigned*>(dst) + e, __float_as_uint(m[e]));
+    }
+  }
+}
+
 // ABL (variants for tools/convbench): 1 = no DMA in the K loop (ablation), 2 = software-
 // pipelined fragment reads (compute_pipe), 4 = s_setprio 1 for the second half of the waves.
 // MF: 0 = v_mfma_f32_32x32x16_f16 (32-row / 32-column wave sub-tiles), 1 = v_mfma_f32_16x16x32_f16
@@ -154,8 +225,11 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
   constexpr int NB_REM = ND_B % NW;  // if != 0: waves < NB_REM issue NB W DMAs, the rest NB - 1
   constexpr int HCH = BM < 128 ? BM : 128;
   constexpr int HEAD_BYTES = EPI == EPI_HEAD ? HCH * 65 * 4 : 0;
-  constexpr int LDS_BYTES = NSTAGE * STAGE > HEAD_BYTES ? NSTAGE * STAGE : HEAD_BYTES;
+  constexpr int POOL_BYTES = EPI == EPI_POOL ? BM * (BN + 4) * 4 + 2 * NW * 4 : 0;
+  constexpr int LDS_A = NSTAGE * STAGE > HEAD_BYTES ? NSTAGE * STAGE : HEAD_BYTES;
+  constexpr int LDS_BYTES = LDS_A > POOL_BYTES ? LDS_A : POOL_BYTES;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+  static_assert(EPI != EPI_POOL || ((BM == 128 || BM == 256) && MF == 0), "pool epilogue: (BM/16)x16 tiles");
 
   // 16x16x32 reads: lane l takes row l & 15, quads / chunk by l >> 4; the extra XOR terms
   // make the ds_read_b128 lane groups {0-3,12-15,20-27}, ... hit 16 distinct bank quads
@@ -198,10 +272,20 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
     const int m = m0 + A_RPD * (wave + NW * i) + arow_in;
     const bool ok = m < M;
     const int mm = ok ? m : 0;
-    const int ow = mm % a.OW;
-    const int t = mm / a.OW;
-    const int oh = t % a.OH;
-    const int b = t / a.OH;
+    int ow, oh, b;
+    if constexpr (EPI == EPI_POOL) {  // block = one (BM/16)x16 tile of a frame, raster order
+      const int P = a.OH * a.OW;
+      b = mm / P;
+      const int rem = mm - b * P, tile = rem / BM, loc = rem % BM, tw_n = a.OW >> 4;
+      const int th = tile / tw_n;
+      oh = th * (BM / 16) + (loc >> 4);
+      ow = ((tile - th * tw_n) << 4) + (loc & 15);
+    } else {
+      ow = mm % a.OW;
+      const int t = mm / a.OW;
+      oh = t % a.OH;
+      b = t / a.OH;
+    }
 #pragma unroll
     for (int sg = 0; sg < NSEG; ++sg) {
       const ConvSeg& g = a.seg[sg];
@@ -501,7 +585,9 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
     return;
   }
   __syncthreads();
-  if constexpr (MF == 1)
+  if constexpr (EPI == EPI_POOL)
+    h3_pool_epilogue<BM, BN, WM, TM, TN, NT>(a, acc, smem, m0, wave, tid, ainv);
+  else if constexpr (MF == 1)
     h3_epilogue16<BM, BN, WM, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wave, tid, ainv);
   else
     x6_epilogue<BM, BN, WM, BN, TM, TN, NT, EPI, 1>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);

@@ -618,13 +618,21 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   }
   const int H2 = H / 2, W2 = W / 2;
   // stem conv7x7/s2/p3 + BN + ReLU   (fpn_resnet.py:179-181)
+  // fp16x3 with an 8x16-tileable stem output: the max-pool (:182) runs in the stem's epilogue
+  // (pooled buffer zeroed first: its tile-border cells are combined with atomicMax)
+  const bool pool_fused = h3 && H2 % 8 == 0 && W2 % 16 == 0;
   {
-    ConvArgs a = conv_args(wb, p.stem, B, H2, W2, F(bf.s0), nullptr, 1);
+    ConvArgs a = conv_args(wb, p.stem, B, H2, W2, pool_fused ? F(bf.p0) : F(bf.s0), nullptr, 1);
     a.seg[0] = seg(xin, B, H, W, 4, 7, 2, 3);
     io(a, AM_INPUT, -1, AM_STEM);
-    SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+    if (pool_fused) {
+      SFA_HIP_TRY(hipMemsetAsync(F(bf.p0), 0, (size_t)B * (H2 / 2) * (W2 / 2) * 64 * sizeof(float), st));
+      SFA_RC(launch_conv(a, EPI_POOL, m->math, st));
+    } else {
+      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+    }
   }
-  SFA_RC(launch_maxpool3s2(F(bf.s0), F(bf.p0), B, H2, W2, 64, st));  // :182
+  if (!pool_fused) SFA_RC(launch_maxpool3s2(F(bf.s0), F(bf.p0), B, H2, W2, 64, st));  // :182
   // residual layers (fpn_resnet.py:184-187)
   const float* xcur = F(bf.p0);
   int xslot = AM_STEM;  // maxpool keeps the stem's max
