@@ -164,7 +164,33 @@ struct ConvArgs {
   float* part;
   size_t part_floats;
   int ksplit;
+  // fp16x3 (conv_h3_kernel) K-slice of a wider packed conv: the fp16 terms' row stride is
+  // wstride (0: Kpad) and the slice starts at K column wk0. Used by the FPN 1x1 convs, which
+  // run their two K-segments as two convs at different resolutions (model.hip).
+  int wstride, wk0;
+  // EPI_STD: residual given at HALF resolution [B][OH/2][OW/2][N], added bilinearly
+  // upsampled x2 (align_corners, source step res_sh / res_sw), or null. bias may be null.
+  const float* res_up;
+  float res_sh, res_sw;
 };
+
+// Bilinear x2 (align_corners) sample of a half-resolution NHWC tensor at output pixel
+// (b, oh, ow), channel n — F.interpolate(scale_factor=2, mode='bilinear', align_corners=True)
+// as upsample2x_bilinear_kernel evaluates it.
+__device__ __forceinline__ float res_up_sample(const ConvArgs& a, int m, int n) {
+  const int ow = m % a.OW, t = m / a.OW;
+  const int oh = t % a.OH, b = t / a.OH;
+  const int H = a.OH >> 1, W = a.OW >> 1;
+  const float fy = a.res_sh * (float)oh, fx = a.res_sw * (float)ow;
+  const int y0 = (int)fy, x0 = (int)fx;
+  const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+  const float ly1 = fy - (float)y0, lx1 = fx - (float)x0;
+  const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+  const float* r = a.res_up + (size_t)b * H * W * a.N + n;
+  const float a00 = r[(y0 * W + x0) * a.N], a01 = r[(y0 * W + x1) * a.N];
+  const float a10 = r[(y1 * W + x0) * a.N], a11 = r[(y1 * W + x1) * a.N];
+  return ly0 * (lx0 * a00 + lx1 * a01) + ly1 * (lx0 * a10 + lx1 * a11);
+}
 
 int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t stream);
 

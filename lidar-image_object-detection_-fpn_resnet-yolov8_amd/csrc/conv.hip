@@ -51,7 +51,8 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;
   auto ok = [](int rc) { return rc != SFA_E_UNSUPPORTED; };
   int rc = SFA_E_UNSUPPORTED;
-  const bool strip = strip_ok(a);
+  const bool sliced = a.wstride || a.wk0 || a.res_up;  // conv_h3_kernel reads these; the others do not
+  const bool strip = strip_ok(a) && !sliced;
   if (epilogue == EPI_HEAD) {
     if (a.N == 320) {
       rc = launch_conv_h3_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2, 1>(a, st);
@@ -64,12 +65,12 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     if (strip) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 2>(a, st);
     if (!ok(rc) && a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 64, 32, EPI_STD, 2, 16, 3, false, 0>(a, st);
-    if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_STD, 1, 16, 3, 0, 64, 1>(a, st);
+    if (!ok(rc) && !sliced) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_STD, 1, 16, 3, 0, 64, 1>(a, st);
     return rc;
   }
   if (a.N % 128 == 0) {
     ConvArgs b = a;
-    b.ksplit = a.part && a.N >= 512 ? 2 : 1;
+    b.ksplit = a.part && a.N >= 512 && !sliced && a.bias ? 2 : 1;
     if (strip) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
     if (!ok(rc) && b.ksplit > 1) {  // K not divisible into the slices: no split
@@ -77,7 +78,7 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
       if (strip) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
       if (!ok(rc)) rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
     }
-    if (!ok(rc)) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2, 16, 3, 0, 128, 1>(b, st);
+    if (!ok(rc) && !sliced) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2, 16, 3, 0, 128, 1>(b, st);
   }
   return rc;
 }
@@ -106,6 +107,17 @@ int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t st) {
   if (a.nseg == 2 && (a.kseg1 % 16 != 0 || a.kseg1 <= 0 || a.kseg1 >= a.Kpad)) {
     set_error("conv: bad kseg1 %d", a.kseg1);
     return SFA_E_UNSUPPORTED;
+  }
+  if (a.wstride || a.wk0 || a.res_up) {  // K-sliced weights / half-res residual: conv_h3_kernel only
+    if (math != SFA_MATH_FP16X3 || epilogue != EPI_STD) {
+      set_error("conv: K-sliced weights / upsampled residual need fp16x3 and the standard epilogue");
+      return SFA_E_UNSUPPORTED;
+    }
+    if (a.res_up && (a.OH % 2 || a.OW % 2 || a.res)) {
+      set_error("conv: upsampled residual needs even output dims and no full-res residual");
+      return SFA_E_UNSUPPORTED;
+    }
+    return launch_conv_h3(a, epilogue, st);
   }
   if (epilogue == EPI_POOL) {  // fused stem + max-pool: fp16x3 only; the caller falls back
     if (math != SFA_MATH_FP16X3 || !a.wh || !a.winv || a.nseg != 1 || a.N != 64 || !a.relu || a.res ||

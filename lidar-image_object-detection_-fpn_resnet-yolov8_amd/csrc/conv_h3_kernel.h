@@ -57,10 +57,21 @@ __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[
             rv[mi][ni][v] = a.res[(size_t)m * a.N + n0 + ni * 16 + c16];
           }
     }
+    if (a.res_up) {
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int m = min(m0 + wave * WM + mi * 16 + 4 * g + v, M - 1);
+            rv[mi][ni][v] = res_up_sample(a, m, n0 + ni * 16 + c16);
+          }
+    }
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
       const int n = n0 + ni * 16 + c16;
-      const float bn = a.bias[n];
+      const float bn = a.bias ? a.bias[n] : 0.f;
       const float cs = a.winv[n];
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
@@ -69,7 +80,7 @@ __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[
           const int m = m0 + wave * WM + mi * 16 + 4 * g + v;
           if (m < M) {
             float val = acc[mi][ni][v] * rinv[mi][v] * cs + bn;
-            if (a.res) val += rv[mi][ni][v];
+            if (a.res || a.res_up) val += rv[mi][ni][v];
             if (a.relu) val = fmaxf(val, 0.f);
             a.y[(size_t)m * a.N + n] = val;
             if (a.amax_out) am.add(a.amax_out, m, val);
@@ -301,7 +312,8 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
       const_cast<float*>(a.seg[NSEG - 1].x), (short)0, (int)a.seg[NSEG - 1].bytes, 0x00020000);
 
   // ---- W DMA slots: groups e = wave + NW * j (term e / ND_BT, rows (e % ND_BT) * B_RPD + ..) ----
-  const unsigned term_bytes = (unsigned)a.N * (unsigned)a.Kpad * 2u;
+  const int wst = a.wstride ? a.wstride : a.Kpad;  // row stride of the fp16 terms
+  const unsigned term_bytes = (unsigned)a.N * (unsigned)wst * 2u;
   const __amdgpu_buffer_rsrc_t rsw =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.wh), (short)0, (int)(2 * term_bytes), 0x00020000);
   constexpr int CPR = BROW / 16;
@@ -312,7 +324,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
     const int t = e / ND_BT;
     const int R = (e % ND_BT) * B_RPD + lane / CPR;
     const int lc = (lane % CPR) ^ swzB(R);
-    boff[j] = (int)(t * term_bytes) + (int)(((n0 + R) * a.Kpad + 8 * lc) << 1);
+    boff[j] = (int)(t * term_bytes) + (int)(((n0 + R) * wst + a.wk0 + 8 * lc) << 1);
   }
 
   // fp16x3 scale of the frame of this lane's A row in each 32-row MFMA tile
@@ -627,7 +639,11 @@ inline int launch_conv_h3_cfg(const ConvArgs& a, hipStream_t st) {
               a.kseg1, a.N);
     return SFA_E_UNSUPPORTED;
   }
-  if (2ull * a.N * a.Kpad * 2ull >= (1ull << 31)) {
+  if (a.wstride && (a.wstride < a.wk0 + a.Kpad || a.wk0 % 8 != 0)) {
+    set_error("conv_h3: K slice [%d, %d) outside the weight rows (stride %d)", a.wk0, a.wk0 + a.Kpad, a.wstride);
+    return SFA_E_INVALID;
+  }
+  if (2ull * a.N * (a.wstride ? a.wstride : a.Kpad) * 2ull >= (1ull << 31)) {
     set_error("conv_h3: split weights >= 2 GiB");
     return SFA_E_UNSUPPORTED;
   }

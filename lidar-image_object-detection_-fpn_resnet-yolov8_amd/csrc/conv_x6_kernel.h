@@ -93,10 +93,21 @@ __device__ __forceinline__ void x6_epilogue(const ConvArgs& a, x6_f32x16 (&acc)[
             rv[mi][ni][v] = a.res[(size_t)m * a.N + n0 + wn * WN + ni * 32 + r];
           }
     }
+    if (a.res_up) {
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+          for (int v = 0; v < 16; ++v) {
+            const int m = min(m0 + wm * WM + mi * 32 + (v & 3) + 8 * (v >> 2) + 4 * h, M - 1);
+            rv[mi][ni][v] = res_up_sample(a, m, n0 + wn * WN + ni * 32 + r);
+          }
+    }
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
       const int n = n0 + wn * WN + ni * 32 + r;
-      const float bn = a.bias[n];
+      const float bn = a.bias ? a.bias[n] : 0.f;
       const float cs = PREC ? a.winv[n] : 1.f;
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
@@ -105,7 +116,7 @@ __device__ __forceinline__ void x6_epilogue(const ConvArgs& a, x6_f32x16 (&acc)[
           const int m = m0 + wm * WM + mi * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
           if (m < M) {
             float val = (PREC ? acc[mi][ni][v] * rinv[mi][v] * cs : acc[mi][ni][v]) + bn;
-            if (a.res) val += rv[mi][ni][v];
+            if (a.res || a.res_up) val += rv[mi][ni][v];
             if (a.relu) val = fmaxf(val, 0.f);
             a.y[(size_t)m * a.N + n] = val;
             if (a.amax_out) am.add(a.amax_out, m, val);

@@ -5,6 +5,8 @@
 //            models/model_utils.py:25-43 (create_model).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstring>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -280,6 +282,8 @@ struct sfa_model {
   const float* w;
   Plan plan;
   int math;
+  int fpn_commute = 7;  // fp16x3: bit f -> FPN conv f as up(W_a x) + W_b skip (env SFA_FPN_COMMUTE, mask)
+  bool pool_fusion = true;  // fp16x3 stem + max-pool in one kernel (env SFA_STEM_POOL_FUSION=0: off)
   // Side stream for the level-0 heads (they only need up_level2, so they overlap the rest
   // of the FPN and the level-1/2 heads); created with the model on the current device,
   // used only when the forward's stream is on that device.
@@ -427,6 +431,8 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   m->w = packed_device;
   m->plan = make_plan(arch);
   m->math = SFA_MATH_FP16X3;
+  if (const char* e = getenv("SFA_STEM_POOL_FUSION")) m->pool_fusion = strcmp(e, "0") != 0;
+  if (const char* e = getenv("SFA_FPN_COMMUTE")) m->fpn_commute = atoi(e) & 7;
   if (hipGetDevice(&m->device) != hipSuccess ||
       hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&m->fork, hipEventDisableTiming) != hipSuccess ||
@@ -620,7 +626,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   // stem conv7x7/s2/p3 + BN + ReLU   (fpn_resnet.py:179-181)
   // fp16x3 with an 8x16-tileable stem output: the max-pool (:182) runs in the stem's epilogue
   // (pooled buffer zeroed first: its tile-border cells are combined with atomicMax)
-  const bool pool_fused = h3 && H2 % 8 == 0 && W2 % 16 == 0;
+  const bool pool_fused = h3 && m->pool_fusion && H2 % 8 == 0 && W2 % 16 == 0;
   {
     ConvArgs a = conv_args(wb, p.stem, B, H2, W2, pool_fused ? F(bf.p0) : F(bf.s0), nullptr, 1);
     a.seg[0] = seg(xin, B, H, W, 4, 7, 2, 3);
@@ -684,15 +690,52 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   // FPN top-down (fpn_resnet.py:197-210): bilinear x2 (align_corners) + channel
   // concat, read by the 1x1 conv as two K-segments (no concat buffer).
   const int H4 = H / 4, W4 = W / 4, H8 = H / 8, W8 = W / 8, H16 = H / 16, W16 = W / 16;
-  SFA_RC(launch_upsample2x(F(bf.l[3]), F(bf.up1), B, H / 32, W / 32, 512, st));
-  {
-    ConvArgs a = conv_args(wb, p.fpn[0], B, H16, W16, F(bf.c1), nullptr, 0);
-    a.nseg = 2;
-    a.kseg1 = 512;
-    a.seg[0] = seg(F(bf.up1), B, H16, W16, 512, 1, 1, 0);
-    a.seg[1] = seg(F(bf.l[2]), B, H16, W16, 256, 1, 1, 0);
-    io(a, blk_slot(3, 1, 1), blk_slot(2, 1, 1), AM_FPN + 0);  // up1 = upsample(layer4)
-    SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+  // fp16x3: each FPN 1x1 conv over cat(up(x), skip) runs as two convs on K-slices of its
+  // packed weights, W_a up(x) + W_b skip + b = up(W_a x) + W_b skip + b (bilinear resize and a
+  // 1x1 conv commute; the interpolation weights sum to 1): W_a x at the LOW resolution into a
+  // half-res buffer (no bias), then W_b skip + b with that buffer added bilinearly upsampled in
+  // the epilogue. A quarter of W_a's MACs, and up_level1 is never materialised.
+  auto commute_at = [&](int f) { return h3 && ((m->fpn_commute >> f) & 1); };
+  float* fpn_lo[3] = {F(bf.up1), F(bf.up1) + (size_t)B * (H / 32) * (W / 32) * 256,
+                      F(bf.up1) + (size_t)B * (H / 32) * (W / 32) * 256 + (size_t)B * H16 * W16 * 128};
+  auto fpn_pair = [&](int f, const float* x, int xh, int xw, int xc, int xslot_in, const float* skip, int sc,
+                      int skip_slot, float* out, int out_slot) -> int {
+    const PConv& pc = p.fpn[f];
+    {
+      ConvArgs a = conv_args(wb, pc, B, xh, xw, fpn_lo[f], nullptr, 0);
+      a.bias = nullptr;
+      a.Kpad = xc;
+      a.wstride = pc.Kpad;
+      a.wk0 = 0;
+      a.seg[0] = seg(x, B, xh, xw, xc, 1, 1, 0);
+      io(a, xslot_in, -1, -1);
+      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+    }
+    ConvArgs a = conv_args(wb, pc, B, 2 * xh, 2 * xw, out, nullptr, 0);
+    a.Kpad = sc;
+    a.wstride = pc.Kpad;
+    a.wk0 = xc;
+    a.seg[0] = seg(skip, B, 2 * xh, 2 * xw, sc, 1, 1, 0);
+    a.res_up = fpn_lo[f];
+    a.res_sh = xh > 1 ? (float)(xh - 1) / (float)(2 * xh - 1) : 0.f;
+    a.res_sw = xw > 1 ? (float)(xw - 1) / (float)(2 * xw - 1) : 0.f;
+    io(a, skip_slot, -1, out_slot);
+    return launch_conv(a, EPI_STD, m->math, st);
+  };
+  if (commute_at(0)) {
+    SFA_RC(fpn_pair(0, F(bf.l[3]), H / 32, W / 32, 512, blk_slot(3, 1, 1), F(bf.l[2]), 256, blk_slot(2, 1, 1),
+                    F(bf.c1), AM_FPN + 0));
+  } else {
+    SFA_RC(launch_upsample2x(F(bf.l[3]), F(bf.up1), B, H / 32, W / 32, 512, st));
+    {
+      ConvArgs a = conv_args(wb, p.fpn[0], B, H16, W16, F(bf.c1), nullptr, 0);
+      a.nseg = 2;
+      a.kseg1 = 512;
+      a.seg[0] = seg(F(bf.up1), B, H16, W16, 512, 1, 1, 0);
+      a.seg[1] = seg(F(bf.l[2]), B, H16, W16, 256, 1, 1, 0);
+      io(a, blk_slot(3, 1, 1), blk_slot(2, 1, 1), AM_FPN + 0);  // up1 = upsample(layer4)
+      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+    }
   }
   SFA_RC(launch_upsample2x(F(bf.c1), F(bf.up2), B, H16, W16, 256, st));
   // Detection heads (fpn_resnet.py:219-233): per level all heads in one launch,
@@ -746,6 +789,10 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   } else {
     SFA_RC(launch_head(0, st));
   }
+  if (commute_at(1)) {
+    SFA_RC(fpn_pair(1, F(bf.c1), H16, W16, 256, AM_FPN + 0, F(bf.l[1]), 128, blk_slot(1, 1, 1), F(bf.c2),
+                    AM_FPN + 1));
+  } else
   {
     ConvArgs a = conv_args(wb, p.fpn[1], B, H8, W8, F(bf.c2), nullptr, 0);
     a.nseg = 2;
@@ -756,6 +803,10 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     SFA_RC(launch_conv(a, EPI_STD, m->math, st));
   }
   SFA_RC(launch_upsample2x(F(bf.c2), F(bf.up3), B, H8, W8, 128, st));
+  if (commute_at(2)) {
+    SFA_RC(fpn_pair(2, F(bf.c2), H8, W8, 128, AM_FPN + 1, F(bf.l[0]), 64, blk_slot(0, 1, 1), F(bf.up4),
+                    AM_FPN + 2));
+  } else
   {
     ConvArgs a = conv_args(wb, p.fpn[2], B, H4, W4, F(bf.up4), nullptr, 0);
     a.nseg = 2;

@@ -174,3 +174,40 @@ def test_forward_608_math_modes(golden, gpu, math):
         e = _err(out[h].cpu().numpy(), golden.model[f"e2e/{h}/full"])
         print(f"{math} 608 {h}: max rel err {e:.3g}")
         assert e <= TOL
+
+
+def test_stem_pool_fusion_bit_exact(golden, gpu, monkeypatch):
+    """fp16x3 stem with the max-pool fused into its epilogue (tile-border cells combined by
+    atomicMax) == stem conv + maxpool3s2_kernel, bit for bit over the whole forward."""
+    x = torch.from_numpy(synthetic.synthetic_bev(3, 160, 192, seed=11)).to(gpu)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SFA_STEM_POOL_FUSION", flag)
+        model = make_model(golden, gpu)  # the flag is read when the native model is created
+        model._engine(gpu).set_math(_math("fp16x3"))
+        with torch.no_grad():
+            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(outs[0][h], outs[1][h])
+
+
+def test_fpn_commute_matches_concat_conv(golden, gpu, monkeypatch):
+    """fp16x3 FPN 1x1 convs run as up(W_a x) + W_b skip + b (K-sliced weights, half-res
+    residual upsampled in the epilogue) == the conv over cat(up(x), skip), to f32 rounding;
+    both within the 1e-4 bar of the CPU reference."""
+    from oracle import model_oracle
+    x = torch.from_numpy(synthetic.synthetic_bev(2, 160, 192, seed=13)).to(gpu)
+    outs = []
+    for flag in ("7", "0"):
+        monkeypatch.setenv("SFA_FPN_COMMUTE", flag)
+        model = make_model(golden, gpu)
+        model._engine(gpu).set_math(_math("fp16x3"))
+        with torch.no_grad():
+            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
+    sd = gc.state_dict_np(golden.model)
+    ref = model_oracle.forward(model_oracle.state_dict_torch(sd), x.cpu(), dict(gc.HEADS))
+    for h in gc.HEADS:
+        r = ref[h].numpy()
+        scale = np.maximum(1.0, np.abs(r))
+        assert float(np.max(np.abs(outs[0][h] - outs[1][h]) / scale)) <= 2e-5, h
+        assert float(np.max(np.abs(outs[0][h] - r) / scale)) <= 1e-4, h
