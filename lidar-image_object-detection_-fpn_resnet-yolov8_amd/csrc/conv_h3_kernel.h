@@ -36,7 +36,6 @@ template <int BM, int BN, int WM, int TM, int TN, int NT, int EPI>
 __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
                                               int m0, int n0, int nt, int wave, int tid,
                                               const float (&ainv)[TM]) {
-  constexpr int HCH = BM < 128 ? BM : 128;
   const int M = a.M, lane = tid & 63, c16 = lane & 15, g = lane >> 4;
   float rinv[TM][4];
 #pragma unroll
@@ -91,9 +90,19 @@ __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[
     if (a.amax_out)
       amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1, reinterpret_cast<float*>(smem));
   } else {
+    // All BM rows of one head's ReLU(conv3x3 + b) staged in LDS at once, the block's 1x1
+    // weights beside them (staged once, not re-read from global per output); the 1x1 conv
+    // then runs LPR lanes per row (KPL of the 64 inputs each, shuffle-reduced): two barriers
+    // per head.
     static_assert(BN % 64 == 0, "whole heads per block");
     constexpr int HPB = BN / 64;
-    float* T = reinterpret_cast<float*>(smem);
+    constexpr int LPR = NT / BM, KPL = 64 / LPR;
+    static_assert(NT % BM == 0 && LPR >= 1 && LPR <= 8 && (LPR & (LPR - 1)) == 0, "1x1 lanes per row");
+    float* T = reinterpret_cast<float*>(smem);  // [BM][65]
+    float* WH = T + BM * 65;                    // [HPB][4][64]
+    for (int i = tid; i < HPB * 256; i += NT) WH[i] = a.hw1[nt * HPB * 256 + i];
+    const int prow = tid / LPR, q = tid % LPR;
+    const int pm = m0 + prow;
 #pragma unroll
     for (int hh = 0; hh < HPB; ++hh) {
       const int head = nt * HPB + hh;
@@ -105,34 +114,46 @@ __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[
           hoff = a.hoff[j];
         }
 #pragma unroll
-      for (int c0 = 0; c0 < BM; c0 += HCH) {
+      for (int ni = 4 * hh; ni < 4 * hh + 4; ++ni) {
+        const int col = (ni - 4 * hh) * 16 + c16;  // column within the head
+        const float bn = a.bias[n0 + 64 * hh + col];
+        const float cs = a.winv[n0 + 64 * hh + col];
 #pragma unroll
-        for (int ni = 4 * hh; ni < 4 * hh + 4; ++ni) {
-          const int col = (ni - 4 * hh) * 16 + c16;  // column within the head
-          const float bn = a.bias[n0 + 64 * hh + col];
-          const float cs = a.winv[n0 + 64 * hh + col];
+        for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-          for (int mi = 0; mi < TM; ++mi)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) {
-              const int row = wave * WM + mi * 16 + 4 * g + v - c0;
-              if (row >= 0 && row < HCH) T[row * 65 + col] = fmaxf(acc[mi][ni][v] * rinv[mi][v] * cs + bn, 0.f);
-            }
-        }
-        __syncthreads();
-        for (int idx = tid; idx < HCH * ch; idx += NT) {
-          const int row = idx % HCH, c = idx / HCH;
-          const int m = m0 + c0 + row;
-          if (m >= M) continue;
-          const float* wr = a.hw1 + (head * 4 + c) * 64;
-          float sum = a.hb1[head * 4 + c];
-          const float* tr = T + row * 65;
-#pragma unroll 16
-          for (int k = 0; k < 64; ++k) sum = fmaf(tr[k], wr[k], sum);
-          a.hout[(size_t)(hoff + c) * M + m] = sum;
-        }
-        __syncthreads();
+          for (int v = 0; v < 4; ++v) {
+            const int row = wave * WM + mi * 16 + 4 * g + v;
+            T[row * 65 + col] = fmaxf(acc[mi][ni][v] * rinv[mi][v] * cs + bn, 0.f);
+          }
       }
+      __syncthreads();
+      float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      const float* tr = T + prow * 65 + q * KPL;
+      const float* wq = WH + hh * 256 + q * KPL;
+#pragma unroll
+      for (int k = 0; k < KPL; ++k) {
+        const float t = tr[k];
+        s0 = fmaf(t, wq[k], s0);
+        s1 = fmaf(t, wq[64 + k], s1);
+        s2 = fmaf(t, wq[128 + k], s2);
+        s3 = fmaf(t, wq[192 + k], s3);
+      }
+#pragma unroll
+      for (int o = 1; o < LPR; o <<= 1) {
+        s0 += __shfl_xor(s0, o, 64);
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+        s3 += __shfl_xor(s3, o, 64);
+      }
+      if (q == 0 && pm < M) {
+        const float* hb = a.hb1 + head * 4;
+        float* o = a.hout + (size_t)hoff * M + pm;
+        o[0] = s0 + hb[0];
+        if (ch > 1) o[(size_t)M] = s1 + hb[1];
+        if (ch > 2) o[2 * (size_t)M] = s2 + hb[2];
+        if (ch > 3) o[3 * (size_t)M] = s3 + hb[3];
+      }
+      __syncthreads();
     }
   }
 }
@@ -235,7 +256,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
   constexpr int NB = (ND_B + NW - 1) / NW;
   constexpr int NB_REM = ND_B % NW;  // if != 0: waves < NB_REM issue NB W DMAs, the rest NB - 1
   constexpr int HCH = BM < 128 ? BM : 128;
-  constexpr int HEAD_BYTES = EPI == EPI_HEAD ? HCH * 65 * 4 : 0;
+  constexpr int HEAD_BYTES = EPI != EPI_HEAD ? 0 : MF == 1 ? BM * 65 * 4 + (BN / 64) * 1024 : HCH * 65 * 4;
   constexpr int POOL_BYTES = EPI == EPI_POOL ? BM * (BN + 4) * 4 + 2 * NW * 4 : 0;
   constexpr int LDS_A = NSTAGE * STAGE > HEAD_BYTES ? NSTAGE * STAGE : HEAD_BYTES;
   constexpr int LDS_BYTES = LDS_A > POOL_BYTES ? LDS_A : POOL_BYTES;

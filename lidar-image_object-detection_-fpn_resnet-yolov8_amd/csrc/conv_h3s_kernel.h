@@ -32,8 +32,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
   constexpr int ND_B = W_BYTES / 1024;  // W pieces per k-step (16 rows each)
   constexpr int NS = (ND_S + NW - 1) / NW, NS_REM = ND_S % NW;
   constexpr int NB = (ND_B + NW - 1) / NW, NB_REM = ND_B % NW;
-  constexpr int HCH = BM < 128 ? BM : 128;
-  constexpr int HEAD_BYTES = EPI == EPI_HEAD ? HCH * 65 * 4 : 0;
+  constexpr int HEAD_BYTES = EPI == EPI_HEAD ? BM * 65 * 4 + (BN / 64) * 1024 : 0;  // h3_epilogue16
   constexpr int MAIN_BYTES = 2 * S_BYTES + 2 * W_BYTES;
   constexpr int LDS_BYTES = MAIN_BYTES > HEAD_BYTES ? MAIN_BYTES : HEAD_BYTES;
   static_assert(NW % 2 == 0 && WM % 16 == 0 && BN % 16 == 0, "tile");
