@@ -1,5 +1,7 @@
 // Convolution dispatch: picks the kernel (f32 MFMA or bf16x6) and its tile
 // configuration per layer shape (conv_kernel.h, conv_x6_kernel.h).
+#include <cstdlib>
+
 #include "conv_kernel.h"
 #include "conv_x6_kernel.h"
 #include "conv_h3_kernel.h"
@@ -41,12 +43,25 @@ static bool strip_ok(const ConvArgs& a) {
 // r01_convbench_h3m.txt, r01_convbench_strip_splitk.txt):
 //  * heads: conv_h3_kernel on 16x16x32 MFMAs, 256x320 (all 5 heads of a level per tile);
 //  * 3x3/s1 body convs: conv_h3s_kernel (A staged once per kh as a row strip for the three kw
-//    taps), 128-row tiles at 2 blocks/CU: -4..5 % vs per-tap staging;
+//    taps): -4..5 % vs per-tap staging; 64-wide: 128x64 at 3 blocks/CU, 128..512-wide: 128x128.
+//    In isolation 64x128 tiles with 16-row wave tiles at 3 blocks/CU are 7-8 % faster on
+//    layer2/3 (profiles/r01_convbench_strip_tiles.txt) and the single-flight forward gains
+//    ~60 us, but with two steps in flight the bench loses ~1 % (profiles/r01_ab_strip_tiles.txt):
+//    kept selectable (SFA_TUNE bit 2), not the default;
 //  * the rest (stride-2 convs, 2-segment convs, 1x1 FPN convs, the stem): conv_h3_kernel,
 //    16x16x32 for the 64-wide ones, 32x32x16 for the 128..512-wide ones, BK 16 for the stem;
 //  * split-K 2 for the 512-wide (layer4) convs, whose 184 tiles cannot fill 256 CUs (-13..16 %);
 //    picked from the width only, so a frame's arithmetic never depends on the batch.
 // conv_x6g_kernel<..., PREC 1> tiles as the fallback.
+// Tuning knob for same-box A/B runs (env SFA_TUNE, read once; 0 = the defaults below).
+static int tune_flags() {
+  static const int f = [] {
+    const char* e = getenv("SFA_TUNE");
+    return e ? atoi(e) : 0;
+  }();
+  return f;
+}
+
 static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;
   auto ok = [](int rc) { return rc != SFA_E_UNSUPPORTED; };
@@ -62,7 +77,10 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     return rc;
   }
   if (a.N == 64) {
-    if (strip) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 2>(a, st);
+    if (strip) {
+      if (tune_flags() & 1) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 2>(a, st);
+      else rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3>(a, st);
+    }
     if (!ok(rc) && a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 64, 32, EPI_STD, 2, 16, 3, false, 0>(a, st);
     if (!ok(rc) && !sliced) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_STD, 1, 16, 3, 0, 64, 1>(a, st);
@@ -71,7 +89,10 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (a.N % 128 == 0) {
     ConvArgs b = a;
     b.ksplit = a.part && a.N >= 512 && !sliced && a.bias ? 2 : 1;
-    if (strip) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
+    if (strip) {
+      if (tune_flags() & 2) rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3>(b, st);
+      else rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
+    }
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
     if (!ok(rc) && b.ksplit > 1) {  // K not divisible into the slices: no split
       b.ksplit = 1;

@@ -209,6 +209,8 @@ int main(int argc, char** argv) {
       {"layer2 3x3 128->128", 16, 76, 76, 128, 3, 1, 1, 128, false, false},
       {"layer3 3x3 256->256", 16, 38, 38, 256, 3, 1, 1, 256, false, false},
       {"layer4 3x3 512->512", 16, 19, 19, 512, 3, 1, 1, 512, false, false},
+      {"s2 layer2.0.conv1 3x3/2 64->128", 16, 152, 152, 64, 3, 2, 1, 128, false, false},
+      {"s2 layer3.0.conv1 3x3/2 128->256", 16, 76, 76, 128, 3, 2, 1, 256, false, false},
       {"head L1 3x3 128->5x64", 16, 152, 152, 128, 3, 1, 1, 320, true, false},
       {"head L2 3x3 64->5x64", 16, 152, 152, 64, 3, 1, 1, 320, true, false},
       {"head L0 3x3 256->5x64", 16, 76, 76, 256, 3, 1, 1, 320, true, false},
@@ -219,6 +221,8 @@ int main(int argc, char** argv) {
       CANDN(256, 64, 32, EPI_STD, 1, 16, 3, false, 0), CANDN(256, 64, 32, EPI_STD, 1, 16, 3, false, 2),
       CANDM(256, 64, 32, EPI_STD, 1, 3, 0), CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
       CANDT(256, 64, 32, EPI_STD, 1, 1), CANDT(128, 64, 32, EPI_STD, 2, 1),
+      CANDT(128, 64, 32, EPI_STD, 3, 1), CANDT(64, 64, 32, EPI_STD, 4, 1), CANDT(64, 64, 16, EPI_STD, 4, 1),
+      CANDT(128, 64, 16, EPI_STD, 2, 1), CANDT(128, 64, 16, EPI_STD, 3, 1), CANDT(256, 64, 16, EPI_STD, 1, 1),
   };
   std::vector<Cand> nbig = {
       CAND(64, 128, 32, 64, 16, EPI_STD, 4),
@@ -227,6 +231,10 @@ int main(int argc, char** argv) {
       CANDK(128, 128, 32, EPI_STD, 2, 2, 2, 0, 8),
       CANDT(128, 128, 32, EPI_STD, 2, 1), CANDT(256, 128, 32, EPI_STD, 1, 1),
       CANDT(128, 128, 32, EPI_STD, 2, 2), CANDT(128, 128, 32, EPI_STD, 2, 4),
+      CANDT(64, 128, 32, EPI_STD, 4, 1), CANDT(64, 128, 16, EPI_STD, 3, 1),
+      CANDT(64, 128, 16, EPI_STD, 3, 2), CANDT(128, 128, 16, EPI_STD, 2, 1), CANDT(128, 128, 16, EPI_STD, 2, 2),
+      CANDT(64, 128, 16, EPI_STD, 2, 1),
+      CANDM(64, 128, 32, EPI_STD, 3, 2, 2), CANDM(128, 128, 32, EPI_STD, 2, 2, 2),
   };
   std::vector<Cand> heads = {
       CAND(128, 64, 32, 64, 16, EPI_HEAD, 4),
