@@ -224,6 +224,12 @@ int main(int argc, char** argv) {
       CANDT(128, 64, 32, EPI_STD, 3, 1), CANDT(64, 64, 32, EPI_STD, 4, 1), CANDT(64, 64, 16, EPI_STD, 4, 1),
       CANDT(128, 64, 16, EPI_STD, 2, 1), CANDT(128, 64, 16, EPI_STD, 3, 1), CANDT(256, 64, 16, EPI_STD, 1, 1),
   };
+  std::vector<Cand> stem = {
+      CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0), CANDN(128, 64, 32, EPI_STD, 3, 16, 3, false, 0),
+      CANDN(128, 64, 32, EPI_STD, 2, 16, 4, false, 0), CANDN(128, 64, 32, EPI_STD, 2, 32, 2, false, 0),
+      CANDM(128, 64, 32, EPI_STD, 2, 2, 2), CANDM(128, 64, 32, EPI_STD, 3, 2, 2), CANDM(128, 64, 32, EPI_STD, 2, 3, 2),
+      CANDM(256, 64, 32, EPI_STD, 1, 2, 2),
+  };
   std::vector<Cand> nbig = {
       CAND(64, 128, 32, 64, 16, EPI_STD, 4),
       CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2), CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 3),
@@ -310,7 +316,7 @@ int main(int argc, char** argv) {
       off += a.hch[j];
     }
     const double flop = 2.0 * M * sh.N * (double)K;
-    std::vector<Cand>& cands = sh.head ? heads : (sh.N == 64 ? n64 : nbig);
+    std::vector<Cand>& cands = sh.head ? heads : sh.C == 4 ? stem : (sh.N == 64 ? n64 : nbig);
     printf("\n== %s  M=%d N=%d K=%d  (%.2f GFLOP)\n", sh.name, M, sh.N, K, flop / 1e9);
     std::vector<float> ref, got;
     for (size_t ci = 0; ci < cands.size(); ++ci) {
