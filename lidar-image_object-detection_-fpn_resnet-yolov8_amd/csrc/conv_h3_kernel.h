@@ -32,10 +32,11 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 // x6_epilogue<..., PREC = 1>: scale back by 1/s of the row's frame and winv[n], bias,
 // residual, ReLU, store, per-frame max |y|; EPI_HEAD stages ReLU(conv3x3 + b) of each head
 // in LDS and applies its 1x1 conv, channel-planar out.
-template <int BM, int BN, int WM, int TM, int TN, int NT, int EPI>
+template <int BM, int BN, int WM, int WN, int TM, int TN, int NT, int EPI>
 __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
-                                              int m0, int n0, int nt, int wave, int tid,
+                                              int m0, int n0, int nt, int wave, int wn, int tid,
                                               const float (&ainv)[TM]) {
+  // wave = the wave's row-block index (wm), wn its column-block index (WN columns each)
   const int M = a.M, lane = tid & 63, c16 = lane & 15, g = lane >> 4;
   float rinv[TM][4];
 #pragma unroll
@@ -53,7 +54,7 @@ __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
             const int m = min(m0 + wave * WM + mi * 16 + 4 * g + v, M - 1);
-            rv[mi][ni][v] = a.res[(size_t)m * a.N + n0 + ni * 16 + c16];
+            rv[mi][ni][v] = a.res[(size_t)m * a.N + n0 + wn * WN + ni * 16 + c16];
           }
     }
     if (a.res_up) {
@@ -64,12 +65,12 @@ __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
             const int m = min(m0 + wave * WM + mi * 16 + 4 * g + v, M - 1);
-            rv[mi][ni][v] = res_up_sample(a, m, n0 + ni * 16 + c16);
+            rv[mi][ni][v] = res_up_sample(a, m, n0 + wn * WN + ni * 16 + c16);
           }
     }
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
-      const int n = n0 + ni * 16 + c16;
+      const int n = n0 + wn * WN + ni * 16 + c16;
       const float bn = a.bias ? a.bias[n] : 0.f;
       const float cs = a.winv[n];
 #pragma unroll
@@ -114,8 +115,10 @@ __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[
           hoff = a.hoff[j];
         }
 #pragma unroll
-      for (int ni = 4 * hh; ni < 4 * hh + 4; ++ni) {
-        const int col = (ni - 4 * hh) * 16 + c16;  // column within the head
+      for (int ni = 0; ni < TN; ++ni) {  // the wave's column blocks that belong to head hh
+        const int gi = wn * TN + ni;
+        if ((gi >> 2) != hh) continue;
+        const int col = (gi - 4 * hh) * 16 + c16;  // column within the head
         const float bn = a.bias[n0 + 64 * hh + col];
         const float cs = a.winv[n0 + 64 * hh + col];
 #pragma unroll
@@ -234,16 +237,20 @@ __device__ __forceinline__ void h3_pool_epilogue(const ConvArgs& a, x6_f32x16 (&
 // MF: 0 = v_mfma_f32_32x32x16_f16 (32-row / 32-column wave sub-tiles), 1 = v_mfma_f32_16x16x32_f16
 // (16 x 16 sub-tiles, BK 32: same LDS reads and registers per MAC; the chip holds a higher
 // clock under the 16x16 shape on random data, MI355X_MICROARCH.md 'DVFS give-back' (7)).
+// WN (16x16x32 form only): columns per wave; WN < BN lays the waves out 2-D, (BM / WM) along M
+// times (BN / WN) along N, so each wave reads WN columns of W fragments instead of all BN
+// (fewer LDS bytes per MAC) and splits its WM rows of A.
 template <int BM, int BN, int WM, int EPI, int OCC, int BK, int NSTAGE, int NSEG, bool NMAJ = false,
-          int ABL = 0, int MF = 0>
-__global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const ConvArgs a) {
+          int ABL = 0, int MF = 0, int WN = BN>
+__global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_h3_kernel(const ConvArgs a) {
   static_assert(BK == 16 || BK == 32, "BK");
   static_assert(NSTAGE >= 2 && NSTAGE <= 4, "ring depth");
   static_assert(NSEG == 1 || NSEG == 2, "segments");
   static_assert(MF == 0 || (BK == 32 && WM % 16 == 0), "16x16x32 form: BK 32");
-  constexpr int NW = BM / WM, NT = NW * 64;
+  static_assert(WN == BN || (MF == 1 && BN % WN == 0 && WN % 16 == 0), "2-D wave layout: 16x16x32 form");
+  constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
   constexpr int MT = MF ? 16 : 32;  // MFMA sub-tile edge
-  constexpr int TM = WM / MT, TN = BN / MT;
+  constexpr int TM = WM / MT, TN = WN / MT;
   constexpr int KST = BK / 16;
   constexpr int AROW = BK * 4, BROW = BK * 2;  // bytes per LDS row
   constexpr int A_BYTES = BM * AROW, TERM_B = BN * BROW;
@@ -274,6 +281,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave % NWM, wn = wave / NWM;  // the wave's row / column block
   const int n_tiles = a.N / BN;
   const int m_tiles = (a.M + BM - 1) / BM;
   const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
@@ -352,7 +360,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
   float as[TM], ainv[TM];
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi) {
-    const int m = min(m0 + wave * WM + mi * MT + (lane & (MT - 1)), M - 1);
+    const int m = min(m0 + wm * WM + mi * MT + (lane & (MT - 1)), M - 1);
     as[mi] = amax_frame_scale(a.amax_in, NSEG, m / (a.OH * a.OW), ainv[mi]);
   }
 
@@ -530,7 +538,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
       f16x8_t hf[2][TM];
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
-        const int R = wave * WM + mi * 16 + c16;
+        const int R = wm * WM + mi * 16 + c16;
         const x6_f32x4 q0 = *reinterpret_cast<const x6_f32x4*>(S + R * AROW + (((2 * g) ^ swzA(R)) << 4));
         const x6_f32x4 q1 = *reinterpret_cast<const x6_f32x4*>(S + R * AROW + (((2 * g + 1) ^ swzA(R)) << 4));
         f16x4_t t0, t1, u0, u1;
@@ -539,7 +547,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
         hf[0][mi] = __builtin_shufflevector(t0, u0, 0, 1, 2, 3, 4, 5, 6, 7);
         hf[1][mi] = __builtin_shufflevector(t1, u1, 0, 1, 2, 3, 4, 5, 6, 7);
       }
-      const unsigned char* SB = S + A_BYTES + c16 * BROW + ((g ^ swzB(c16)) << 4);
+      const unsigned char* SB = S + A_BYTES + (wn * WN + c16) * BROW + ((g ^ swzB(c16)) << 4);
       f16x8_t bq[3][2];
       auto read_b = [&](int ni) {
         bq[ni % 3][0] = *reinterpret_cast<const f16x8_t*>(SB + ni * 16 * BROW);
@@ -612,7 +620,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
             col = ni * 32 + (lane & 31);
           }
           const float si = __shfl(ainv[mi], MF ? (row & 15) : (row & 31), 64);
-          const int m = m0 + wave * WM + row, n = n0 + col;
+          const int m = m0 + wm * WM + row, n = n0 + wn * WN + col;
           if (m < M) part[(size_t)m * a.N + n] = acc[mi][ni][v] * si * a.winv[n];
         }
     return;
@@ -621,7 +629,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3_kernel(const Conv
   if constexpr (EPI == EPI_POOL)
     h3_pool_epilogue<BM, BN, WM, TM, TN, NT>(a, acc, smem, m0, wave, tid, ainv);
   else if constexpr (MF == 1)
-    h3_epilogue16<BM, BN, WM, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wave, tid, ainv);
+    h3_epilogue16<BM, BN, WM, WN, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wm, wn, tid, ainv);
   else
     x6_epilogue<BM, BN, WM, BN, TM, TN, NT, EPI, 1>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
 }
@@ -653,7 +661,7 @@ static __global__ void __launch_bounds__(256) splitk_reduce_kernel(const ConvArg
 }
 
 template <int BM, int BN, int WM, int EPI, int OCC, int BK, int NSTAGE, bool NMAJ = false, int ABL = 0,
-          int MF = 0>
+          int MF = 0, int WN = BN>
 inline int launch_conv_h3_cfg(const ConvArgs& a, hipStream_t st) {
   if (!a.wh || !a.winv || a.Kpad % BK != 0 || (a.nseg == 2 && a.kseg1 % BK != 0) || a.N % BN != 0) {
     set_error("conv_h3: K/N not aligned to the tile or no split weights (Kpad=%d kseg1=%d N=%d)", a.Kpad,
@@ -680,11 +688,11 @@ inline int launch_conv_h3_cfg(const ConvArgs& a, hipStream_t st) {
     return SFA_E_INVALID;
   }
   if (a.nseg == 2)
-    hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 2, NMAJ, ABL, MF>), dim3((unsigned)nblocks),
-                       dim3((BM / WM) * 64), 0, st, a);
+    hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 2, NMAJ, ABL, MF, WN>),
+                       dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WN) * 64), 0, st, a);
   else
-    hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 1, NMAJ, ABL, MF>), dim3((unsigned)nblocks),
-                       dim3((BM / WM) * 64), 0, st, a);
+    hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 1, NMAJ, ABL, MF, WN>),
+                       dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WN) * 64), 0, st, a);
   SFA_LAUNCH_CHECK();
   if (ks > 1) {
     const long long nel = (long long)a.M * a.N;

@@ -214,7 +214,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     return;
   }
   __syncthreads();
-  h3_epilogue16<BM, BN, WM, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wave, tid, ainv);
+  h3_epilogue16<BM, BN, WM, BN, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
 }
 
 template <int BM, int BN, int WM, int EPI, int OCC>

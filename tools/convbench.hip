@@ -173,6 +173,11 @@ struct Cand {
     "h3m " #BM "x" #BN " w" #WM " occ" #OCC " bk32 st" #NS " abl" #ABL, 32,                 \
         [](const ConvArgs& a, hipStream_t s) { return launch_conv_h3_cfg<BM, BN, WM, EPI, OCC, 32, NS, false, ABL, 1>(a, s); } \
   }
+#define CANDW(BM, BN, WM, WN, EPI, OCC, NS, ABL)                                        \
+  Cand {                                                                                \
+    "h3w " #BM "x" #BN " w" #WM "x" #WN " occ" #OCC " bk32 st" #NS " abl" #ABL, 32,         \
+        [](const ConvArgs& a, hipStream_t s) { return launch_conv_h3_cfg<BM, BN, WM, EPI, OCC, 32, NS, false, ABL, 1, WN>(a, s); } \
+  }
 static float* g_part = nullptr;
 static const size_t g_part_floats = 64u << 20;
 #define CANDK(BM, BN, WM, EPI, OCC, NS, ABL, MF, KS)                                                \
@@ -246,6 +251,8 @@ int main(int argc, char** argv) {
       CAND(128, 64, 32, 64, 16, EPI_HEAD, 4),
       CANDM(256, 320, 32, EPI_HEAD, 1, 2, 2), CANDM(256, 320, 32, EPI_HEAD, 1, 2, 3),
       CANDT(256, 320, 32, EPI_HEAD, 1, 1),
+      CANDW(256, 320, 64, 160, EPI_HEAD, 1, 2, 2), CANDW(256, 320, 32, 160, EPI_HEAD, 1, 2, 2),
+      CANDW(128, 320, 32, 160, EPI_HEAD, 1, 2, 2),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
