@@ -193,5 +193,8 @@ __device__ __forceinline__ float res_up_sample(const ConvArgs& a, int m, int n) 
 }
 
 int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t stream);
+// fp16x3 stem 7x7/s2 (NHWC4) + BN + ReLU + max-pool 3x3/s2 from LDS input patches
+// (stem_patch_kernel.h); SFA_E_UNSUPPORTED if the stem's shape does not tile 16 x 16.
+int launch_stem_patch(const ConvArgs& a, hipStream_t stream);
 
 }  // namespace sfa

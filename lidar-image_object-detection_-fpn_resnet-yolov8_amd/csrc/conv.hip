@@ -6,6 +6,7 @@
 #include "conv_x6_kernel.h"
 #include "conv_h3_kernel.h"
 #include "conv_h3s_kernel.h"
+#include "stem_patch_kernel.h"
 
 namespace sfa {
 
@@ -178,5 +179,7 @@ int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t st) {
   }
   return launch_conv_cfg<64, 64, 32, 32, 16, EPI_STD, 4>(a, st);
 }
+
+int launch_stem_patch(const ConvArgs& a, hipStream_t st) { return launch_stem_patch_pool(a, st); }
 
 }  // namespace sfa

@@ -284,6 +284,7 @@ struct sfa_model {
   int math;
   int fpn_commute = 7;  // fp16x3: bit f -> FPN conv f as up(W_a x) + W_b skip (env SFA_FPN_COMMUTE, mask)
   bool pool_fusion = true;  // fp16x3 stem + max-pool in one kernel (env SFA_STEM_POOL_FUSION=0: off)
+  bool stem_patch = true;   // ... from LDS input patches (stem_patch_kernel.h; env SFA_STEM_PATCH=0: off)
   // Side stream for the level-0 heads (they only need up_level2, so they overlap the rest
   // of the FPN and the level-1/2 heads); created with the model on the current device,
   // used only when the forward's stream is on that device.
@@ -432,6 +433,7 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   m->plan = make_plan(arch);
   m->math = SFA_MATH_FP16X3;
   if (const char* e = getenv("SFA_STEM_POOL_FUSION")) m->pool_fusion = strcmp(e, "0") != 0;
+  if (const char* e = getenv("SFA_STEM_PATCH")) m->stem_patch = strcmp(e, "0") != 0;
   if (const char* e = getenv("SFA_FPN_COMMUTE")) m->fpn_commute = atoi(e) & 7;
   if (hipGetDevice(&m->device) != hipSuccess ||
       hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking) != hipSuccess ||
@@ -633,7 +635,10 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     io(a, AM_INPUT, -1, AM_STEM);
     if (pool_fused) {
       SFA_HIP_TRY(hipMemsetAsync(F(bf.p0), 0, (size_t)B * (H2 / 2) * (W2 / 2) * 64 * sizeof(float), st));
-      SFA_RC(launch_conv(a, EPI_POOL, m->math, st));
+      if (m->stem_patch && H2 % 16 == 0 && W2 % 16 == 0)
+        SFA_RC(launch_stem_patch(a, st));
+      else
+        SFA_RC(launch_conv(a, EPI_POOL, m->math, st));
     } else {
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }

@@ -1,0 +1,250 @@
+// Stem conv 7x7/s2/p3 (4 -> 64, NHWC4 input) + BN + ReLU + max-pool 3x3/s2/p1, fp16x3, from
+// an LDS input patch (fpn_resnet.py:179-182).
+//
+// The implicit-GEMM stem (conv_h3_kernel<..., EPI_POOL>) gathers every K-tile of A from L2:
+// 49 taps x 16 B per output pixel. Here a block instead stages, per 16 x 16 tile of the
+// 304 x 304 conv output, the 37 x 38 input pixels its windows cover ONCE, split into two
+// fp16 terms (x s = hi + lo, s the frame's power-of-two scale), and reads every MFMA A
+// fragment from that patch. K is laid out (kh, kw 0..7, c 0..3) = 224 with a zero weight
+// column at kw = 7, so the 8 k values a lane holds (two kw, four channels) are two adjacent
+// patch pixels: one 16-B ds_read per term. The split weights (64 x 224 x 2 terms, 58 KiB)
+// stay in LDS for the block's lifetime; blocks loop over tiles (grid = CUs) and prefetch
+// the next tile's patch into registers while the current tile computes. Epilogue: the
+// stem + pool epilogue of conv_h3_kernel (h3_pool_epilogue, 16 x 16 tiles).
+#pragma once
+
+#include "conv_h3_kernel.h"
+
+namespace sfa {
+
+namespace stem_patch {
+constexpr int TH = 16, TW = 16;                // conv-output tile
+constexpr int PH = 2 * TH + 5, PW = 2 * TW + 6;  // patch: rows 2 oy - 3 + 0..36, cols 2 ox - 3 + 0..37
+constexpr int PIX = PH * PW;                   // 1406
+constexpr int KP = 224;                        // (kh, kw 0..7, c 0..3)
+constexpr int WROW = KP * 2 + 16;              // bytes per W row in LDS (padded: conflict-free b128)
+constexpr int W_BYTES = 2 * 64 * WROW;         // two fp16 terms
+constexpr int PATCH_TERM = PIX * 8;            // 4 fp16 per pixel
+constexpr int NT = 512, NW = 8;
+constexpr int PF = (PIX + NT - 1) / NT;        // patch pixels prefetched per thread (3)
+constexpr int T_BYTES = 256 * (64 + 4) * 4 + 2 * NW * 4;  // h3_pool_epilogue's LDS
+constexpr int LDS_BYTES = W_BYTES + 2 * PATCH_TERM + T_BYTES;  // 151,600 B: one block per CU
+}  // namespace stem_patch
+
+// Epilogue for one 16 x 16 tile (th, tw) of frame b: ReLU(conv * 1/s * winv + b) into LDS,
+// the frame's max recorded, then the 9 x 9 pooled cells whose 3 x 3/s2 window touches the
+// tile (pooled rows 8 th .. 8 th + 8, cols 8 tw .. 8 tw + 8): each thread takes one cell and
+// four channels, its window's nine float4 reads unrolled (indices clamped to the tile: a
+// repeated element does not change a max). Cells with one writer (j, i in 1..7) are stored,
+// the tile-border cells shared with a neighbour combined by atomicMax on the f32 bits
+// (values >= +0) into the zeroed pooled buffer — the same rule as h3_pool_epilogue.
+__device__ __forceinline__ void stem_pool_epilogue(const ConvArgs& a, x6_f32x16 (&acc)[1][2], float* T, int b,
+                                                   int th, int tw, int wave, int tid, float ainv) {
+  constexpr int LD = 68;
+  const int lane = tid & 63, r = lane & 31, h = lane >> 5;
+  float mx = 0.f;
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    const int n = ni * 32 + r;
+    const float bn = a.bias[n];
+    const float cs = a.winv[n] * ainv;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int row = wave * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+      float val = acc[0][ni][v] * cs + bn;
+      val = val > 0.f ? val : 0.f;
+      T[row * LD + n] = val;
+      mx = fmaxf(mx, val);
+    }
+  }
+  if (a.amax_out)
+    amax_commit_block<8>(a.amax_out, b, mx, 0.f, T + 256 * LD);  // includes __syncthreads
+  else
+    __syncthreads();
+  const int PHo = a.OH >> 1, PWo = a.OW >> 1;
+  const int c4 = tid & 15;
+#pragma unroll
+  for (int pass = 0; pass < 3; ++pass) {
+    const int cell = (tid >> 4) + 32 * pass;
+    if (cell >= 81) break;
+    const int j = cell / 9, i = cell - 9 * j;
+    const int py = 8 * th + j, px = 8 * tw + i;
+    if (py >= PHo || px >= PWo) continue;
+    const int ra = max(2 * j - 1, 0), rb = min(2 * j, 15), rc = min(2 * j + 1, 15);
+    const int qa = max(2 * i - 1, 0), qb = min(2 * i, 15), qc = min(2 * i + 1, 15);
+    const int rr[3] = {ra, rb, rc}, qq[3] = {qa, qb, qc};
+    x6_f32x4 m = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int y = 0; y < 3; ++y)
+#pragma unroll
+      for (int x = 0; x < 3; ++x) {
+        const x6_f32x4 t = *reinterpret_cast<const x6_f32x4*>(T + (rr[y] * 16 + qq[x]) * LD + 4 * c4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], t[e]);
+      }
+    float* dst = a.y + ((size_t)(b * PHo + py) * PWo + px) * 64 + 4 * c4;
+    if (j >= 1 && j <= 7 && i >= 1 && i <= 7) {
+      *reinterpret_cast<x6_f32x4*>(dst) = m;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (m[e] > 0.f) atomicMax(reinterpret_cast<unsigned*>(dst) + e, __float_as_uint(m[e]));
+    }
+  }
+}
+
+// ABL (timing ablations only, env SFA_STEM_ABL; results wrong): 1 = no epilogue, 2 = no MFMAs,
+// 4 = no patch fetch
+template <int ABL = 0>
+__global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs a, int ntiles) {
+  using namespace stem_patch;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+  unsigned char* SW = smem;
+  unsigned char* SU = smem + W_BYTES;                   // patch, 2 terms
+  unsigned char* ST = smem + W_BYTES + 2 * PATCH_TERM;  // epilogue tile (its own LDS: no barrier
+                                                        // between a tile's epilogue and the next patch)
+  // LDS-only barrier (the no-return pooled atomics of the previous tile stay in flight)
+  auto lds_barrier = [] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+  const ConvSeg& g = a.seg[0];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tw_n = a.OW / TW, tiles_per_frame = (a.OH / TH) * tw_n;
+
+  // weights: wh [2][64][Kpad] with k = (kh 7 + kw) 4 + c  ->  LDS [2][64][WROW] at k' = (kh 8 + kw) 4 + c
+  for (int i = tid; i < 2 * 64 * 56; i += NT) {
+    const int t = i / (64 * 56), rem = i - t * (64 * 56);
+    const int n = rem / 56, tap = rem - n * 56;
+    const int kh = tap >> 3, kw = tap & 7;
+    uint2 v = make_uint2(0u, 0u);
+    if (kw < 7)
+      v = *reinterpret_cast<const uint2*>(a.wh + ((size_t)t * 64 + n) * a.Kpad + (kh * 7 + kw) * 4);
+    *reinterpret_cast<uint2*>(SW + t * 64 * WROW + n * WROW + tap * 8) = v;
+  }
+
+  x6_f32x4 pf[PF];
+  auto fetch = [&](int tile) {
+    const int b = tile / tiles_per_frame, tl = tile - b * tiles_per_frame;
+    const int th = tl / tw_n, tw = tl - th * tw_n;
+    const int iy0 = 2 * TH * th - 3, ix0 = 2 * TW * tw - 3;
+    const x6_f32x4* x = reinterpret_cast<const x6_f32x4*>(g.x) + (size_t)b * g.H * g.W;
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int p = tid + j * NT;
+      const int py = p / PW, px = p - py * PW;
+      const int iy = iy0 + py, ix = ix0 + px;
+      x6_f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (p < PIX && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W) v = x[iy * g.W + ix];
+      pf[j] = v;
+    }
+  };
+  auto store_patch = [&](float s) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int p = tid + j * NT;
+      if (p < PIX) {
+        f16x4_t hi, lo;
+        split2h(pf[j], s, hi, lo);
+        *reinterpret_cast<f16x4_t*>(SU + p * 8) = hi;
+        *reinterpret_cast<f16x4_t*>(SU + PATCH_TERM + p * 8) = lo;
+      }
+    }
+  };
+
+  const int r = lane & 31, h = lane >> 5;
+  // A fragment origin of this lane: conv-output pixel (oy, ox) = (2 wave + r / 16, r % 16) of the
+  // tile -> patch pixel (2 oy, 2 ox) + (kh, 4 (s & 1) + 2 h) at k-step s
+  const int oyl = 2 * wave + (r >> 4), oxl = r & 15;
+  const int abase = ((2 * oyl) * PW + 2 * oxl + 2 * h) * 8;
+  const int bbase = r * WROW + 16 * h;
+
+  int tile = blockIdx.x;
+  if (tile < ntiles && !(ABL & 4)) fetch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int b = tile / tiles_per_frame;
+    float ainv[1];
+    const float as = amax_frame_scale(a.amax_in, 1, b, ainv[0]);
+    store_patch(as);
+    // patch (and, first time round, the weights) in LDS; every wave is past the previous
+    // tile's epilogue reads of ST
+    lds_barrier();
+    if (tile + (int)gridDim.x < ntiles && !(ABL & 4)) fetch(tile + gridDim.x);  // lands during the MFMAs
+
+    x6_f32x16 acc[1][2];
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int v = 0; v < 16; ++v) acc[0][ni][v] = 0.f;
+#pragma unroll
+    for (int s = 0; s < ((ABL & 2) ? 0 : KP / 16); ++s) {
+      const int aoff = abase + ((s >> 1) * PW + 4 * (s & 1)) * 8;
+      const f16x8_t ahi = *reinterpret_cast<const f16x8_t*>(SU + aoff);
+      const f16x8_t alo = *reinterpret_cast<const f16x8_t*>(SU + PATCH_TERM + aoff);
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const unsigned char* wb = SW + bbase + ni * 32 * WROW + 32 * s;
+        const f16x8_t whi = *reinterpret_cast<const f16x8_t*>(wb);
+        const f16x8_t wlo = *reinterpret_cast<const f16x8_t*>(wb + 64 * WROW);
+        x6_f32x16 cc = acc[0][ni];
+        cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi, cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo, cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi, cc, 0, 0, 0);
+        acc[0][ni] = cc;
+      }
+    }
+    // the epilogue's own barrier (after its ST writes) also orders this tile's patch reads
+    // before the next tile's patch stores
+    if constexpr ((ABL & 1) != 0) {
+      float t = 0.f;
+#pragma unroll
+      for (int v = 0; v < 16; ++v) t += acc[0][0][v] + acc[0][1][v];
+      if (t == 1234.5f) a.y[tid] = t;
+      __syncthreads();
+    } else {
+      const int tl = tile - b * tiles_per_frame, th = tl / tw_n;
+      stem_pool_epilogue(a, acc, reinterpret_cast<float*>(ST), b, th, tl - th * tw_n, wave, tid, ainv[0]);
+    }
+  }
+}
+
+// Grid = one block per CU (each loops over tiles); needs the stem's fp16x3 split weights
+// (Kpad >= 196), NHWC4 input, conv output divisible into 16 x 16 tiles.
+inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
+  const ConvSeg& g = a.seg[0];
+  if (!a.wh || !a.winv || a.nseg != 1 || a.N != 64 || g.C != 4 || g.KH != 7 || g.KW != 7 || g.stride != 2 ||
+      g.pad != 3 || a.Kpad < 196 || a.OH % 16 != 0 || a.OW % 16 != 0 || a.OH * 2 != g.H || a.OW * 2 != g.W ||
+      a.res || !a.relu) {
+    set_error("stem_patch: unsupported stem (C=%d k=%d OH=%d OW=%d)", g.C, g.KH, a.OH, a.OW);
+    return SFA_E_UNSUPPORTED;
+  }
+  const int frames = a.M / (a.OH * a.OW);
+  const int ntiles = frames * (a.OH / 16) * (a.OW / 16);
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  const int grid = ntiles < ncu ? ntiles : ncu;
+  if (grid <= 0) return SFA_OK;
+  static int abl = -1;
+  if (abl < 0) {
+    const char* e = getenv("SFA_STEM_ABL");
+    abl = e ? atoi(e) : 0;
+  }
+  const dim3 gd((unsigned)grid), bd(stem_patch::NT);
+  switch (abl) {
+    case 1: hipLaunchKernelGGL(stem_patch_pool_kernel<1>, gd, bd, 0, st, a, ntiles); break;
+    case 2: hipLaunchKernelGGL(stem_patch_pool_kernel<2>, gd, bd, 0, st, a, ntiles); break;
+    case 4: hipLaunchKernelGGL(stem_patch_pool_kernel<4>, gd, bd, 0, st, a, ntiles); break;
+    case 3: hipLaunchKernelGGL(stem_patch_pool_kernel<3>, gd, bd, 0, st, a, ntiles); break;
+    default: hipLaunchKernelGGL(stem_patch_pool_kernel<0>, gd, bd, 0, st, a, ntiles); break;
+  }
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+}  // namespace sfa

@@ -181,6 +181,7 @@ def test_stem_pool_fusion_bit_exact(golden, gpu, monkeypatch):
     atomicMax) == stem conv + maxpool3s2_kernel, bit for bit over the whole forward."""
     x = torch.from_numpy(synthetic.synthetic_bev(3, 160, 192, seed=11)).to(gpu)
     outs = []
+    monkeypatch.setenv("SFA_STEM_PATCH", "0")  # the implicit-GEMM stem (same K order as unfused)
     for flag in ("1", "0"):
         monkeypatch.setenv("SFA_STEM_POOL_FUSION", flag)
         model = make_model(golden, gpu)  # the flag is read when the native model is created
@@ -189,6 +190,32 @@ def test_stem_pool_fusion_bit_exact(golden, gpu, monkeypatch):
             outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
     for h in gc.HEADS:
         np.testing.assert_array_equal(outs[0][h], outs[1][h])
+
+
+@pytest.mark.parametrize("hw", [(160, 192), (608, 608)])
+def test_stem_patch_matches_gather_stem(golden, gpu, monkeypatch, hw):
+    """fp16x3 stem + pool from LDS input patches (stem_patch_kernel.h: K laid out with kw
+    padded to 8, so its f32 sums run in a different order) == the implicit-GEMM fused stem
+    to f32 rounding; both within the 1e-4 bar of the CPU reference."""
+    from oracle import model_oracle
+    x = torch.from_numpy(synthetic.synthetic_bev(2, hw[0], hw[1], seed=17)).to(gpu)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SFA_STEM_PATCH", flag)
+        model = make_model(golden, gpu)
+        model._engine(gpu).set_math(_math("fp16x3"))
+        with torch.no_grad():
+            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
+    sd = gc.state_dict_np(golden.model)
+    ref = model_oracle.forward(model_oracle.state_dict_torch(sd), x.cpu(), dict(gc.HEADS))
+    for h in gc.HEADS:
+        r = ref[h].numpy()
+        scale = np.maximum(1.0, np.abs(r))
+        d = float(np.max(np.abs(outs[0][h] - outs[1][h]) / scale))
+        e = float(np.max(np.abs(outs[0][h] - r) / scale))
+        print(f"stem patch {hw} {h}: vs gather stem {d:.3g}, vs reference {e:.3g}")
+        assert d <= 2e-5, h
+        assert e <= 1e-4, h
 
 
 def test_fpn_commute_matches_concat_conv(golden, gpu, monkeypatch):
