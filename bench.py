@@ -445,7 +445,9 @@ def main():
                 "bound": "mfma",
                 "kernel": {"f32": "conv_mfma_kernel", "bf16x6": "conv_x6_kernel / conv_x6g_kernel",
                            "fp16x3": "conv_h3_kernel"}.get(args.math, args.math) + " (math %s)" % args.math +
-                          " (23 implicit-GEMM launches per forward; achieved = algorithmic f32 FLOP "
+                          (" (22 implicit-GEMM launches + the LDS-patch stem" if args.math == "fp16x3"
+                           else " (23 implicit-GEMM launches") +
+                          " per forward; achieved = algorithmic f32 FLOP "
                           "over the whole forward's event time, aux kernels included)",
                 "achieved": round(achieved, 3),
                 "peak": round(peak, 2),
