@@ -94,7 +94,7 @@ __device__ __forceinline__ void stem_pool_epilogue(const ConvArgs& a, x6_f32x16 
 }
 
 // ABL (timing ablations only, env SFA_STEM_ABL; results wrong): 1 = no epilogue, 2 = no MFMAs,
-// 4 = no patch fetch
+// 4 = no patch fetch, 8 = first patch fetched after the weights are staged
 template <int ABL = 0>
 __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs a, int ntiles) {
   using namespace stem_patch;
@@ -112,17 +112,6 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tw_n = a.OW / TW, tiles_per_frame = (a.OH / TH) * tw_n;
-
-  // weights: wh [2][64][Kpad] with k = (kh 7 + kw) 4 + c  ->  LDS [2][64][WROW] at k' = (kh 8 + kw) 4 + c
-  for (int i = tid; i < 2 * 64 * 56; i += NT) {
-    const int t = i / (64 * 56), rem = i - t * (64 * 56);
-    const int n = rem / 56, tap = rem - n * 56;
-    const int kh = tap >> 3, kw = tap & 7;
-    uint2 v = make_uint2(0u, 0u);
-    if (kw < 7)
-      v = *reinterpret_cast<const uint2*>(a.wh + ((size_t)t * 64 + n) * a.Kpad + (kh * 7 + kw) * 4);
-    *reinterpret_cast<uint2*>(SW + t * 64 * WROW + n * WROW + tap * 8) = v;
-  }
 
   x6_f32x4 pf[PF];
   auto fetch = [&](int tile) {
@@ -161,7 +150,20 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs 
   const int bbase = r * WROW + 16 * h;
 
   int tile = blockIdx.x;
-  if (tile < ntiles && !(ABL & 4)) fetch(tile);
+  if (tile < ntiles && !(ABL & 4) && !(ABL & 8)) fetch(tile);  // in flight while the weights are staged
+  // weights: wh [2][64][Kpad] with k = (kh 7 + kw) 4 + c  ->  LDS [2][64][WROW] at k' = (kh 8 + kw) 4 + c
+#pragma unroll
+  for (int i = tid; i < 2 * 64 * 56; i += NT) {
+    const int t = i / (64 * 56), rem = i - t * (64 * 56);
+    const int n = rem / 56, tap = rem - n * 56;
+    const int kh = tap >> 3, kw = tap & 7;
+    uint2 v = make_uint2(0u, 0u);
+    if (kw < 7)
+      v = *reinterpret_cast<const uint2*>(a.wh + ((size_t)t * 64 + n) * a.Kpad + (kh * 7 + kw) * 4);
+    *reinterpret_cast<uint2*>(SW + t * 64 * WROW + n * WROW + tap * 8) = v;
+  }
+
+  if (tile < ntiles && !(ABL & 4) && (ABL & 8)) fetch(tile);
   for (; tile < ntiles; tile += gridDim.x) {
     const int b = tile / tiles_per_frame;
     float ainv[1];
@@ -241,6 +243,7 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
     case 2: hipLaunchKernelGGL(stem_patch_pool_kernel<2>, gd, bd, 0, st, a, ntiles); break;
     case 4: hipLaunchKernelGGL(stem_patch_pool_kernel<4>, gd, bd, 0, st, a, ntiles); break;
     case 3: hipLaunchKernelGGL(stem_patch_pool_kernel<3>, gd, bd, 0, st, a, ntiles); break;
+    case 8: hipLaunchKernelGGL(stem_patch_pool_kernel<8>, gd, bd, 0, st, a, ntiles); break;
     default: hipLaunchKernelGGL(stem_patch_pool_kernel<0>, gd, bd, 0, st, a, ntiles); break;
   }
   SFA_LAUNCH_CHECK();
