@@ -633,12 +633,15 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     ConvArgs a = conv_args(wb, p.stem, B, H2, W2, pool_fused ? F(bf.p0) : F(bf.s0), nullptr, 1);
     a.seg[0] = seg(xin, B, H, W, 4, 7, 2, 3);
     io(a, AM_INPUT, -1, AM_STEM);
-    if (pool_fused) {
+    if (pool_fused && m->stem_patch && H2 % 16 == 0 && W2 % 16 == 0) {
+      // every pooled cell has one owner tile; the tile-border parts of the neighbours go
+      // through the (here unused) unfused stem buffer and a merge pass: no memset, no atomics
+      a.part = F(bf.s0);
+      a.part_floats = (size_t)B * H2 * W2 * 64;
+      SFA_RC(launch_stem_patch(a, st));
+    } else if (pool_fused) {
       SFA_HIP_TRY(hipMemsetAsync(F(bf.p0), 0, (size_t)B * (H2 / 2) * (W2 / 2) * 64 * sizeof(float), st));
-      if (m->stem_patch && H2 % 16 == 0 && W2 % 16 == 0)
-        SFA_RC(launch_stem_patch(a, st));
-      else
-        SFA_RC(launch_conv(a, EPI_POOL, m->math, st));
+      SFA_RC(launch_conv(a, EPI_POOL, m->math, st));
     } else {
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }

@@ -38,6 +38,7 @@ constexpr int LDS_BYTES = W_BYTES + 2 * PATCH_TERM + T_BYTES;  // 151,600 B: one
 // repeated element does not change a max). Cells with one writer (j, i in 1..7) are stored,
 // the tile-border cells shared with a neighbour combined by atomicMax on the f32 bits
 // (values >= +0) into the zeroed pooled buffer — the same rule as h3_pool_epilogue.
+template <bool NOATOM = false>
 __device__ __forceinline__ void stem_pool_epilogue(const ConvArgs& a, x6_f32x16 (&acc)[1][2], float* T, int b,
                                                    int th, int tw, int wave, int tid, float ainv) {
   constexpr int LD = 68;
@@ -83,7 +84,15 @@ __device__ __forceinline__ void stem_pool_epilogue(const ConvArgs& a, x6_f32x16 
         for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], t[e]);
       }
     float* dst = a.y + ((size_t)(b * PHo + py) * PWo + px) * 64 + 4 * c4;
-    if (j >= 1 && j <= 7 && i >= 1 && i <= 7) {
+    if (a.part) {  // side-buffer mode: cells j, i <= 7 are this tile's own, the rest go to its slots
+      if (j <= 7 && i <= 7) {
+        *reinterpret_cast<x6_f32x4*>(dst) = m;
+      } else {
+        const int slot = j == 8 ? i : 9 + j;
+        const int tl = (b * (a.OH >> 4) + th) * (a.OW >> 4) + tw;
+        *reinterpret_cast<x6_f32x4*>(a.part + ((size_t)tl * 17 + slot) * 64 + 4 * c4) = m;
+      }
+    } else if (NOATOM || (j >= 1 && j <= 7 && i >= 1 && i <= 7)) {
       *reinterpret_cast<x6_f32x4*>(dst) = m;
     } else {
 #pragma unroll
@@ -93,8 +102,42 @@ __device__ __forceinline__ void stem_pool_epilogue(const ConvArgs& a, x6_f32x16 
   }
 }
 
+// Side-buffer mode (a.part != null): every pooled cell has ONE owner tile, the tile holding
+// conv pixel (2 py, 2 px); it stores its part of the window (rows/cols inside the tile) with a
+// plain store. A tile's parts of its lower / right neighbours' cells (its pooled row j = 8 and
+// column i = 8, 17 slots x 64 channels) go to a.part, and this kernel merges them into the
+// owners' top-row / left-column cells: the up tile's row slot, the left tile's column slot,
+// the up-left tile's corner slot — max is order-free, so the result equals the atomicMax form
+// bit for bit, without 2,048 atomics per tile and without zeroing the pooled buffer first.
+__global__ void __launch_bounds__(256) stem_pool_merge_kernel(const ConvArgs a, int frames) {
+  const int tr = a.OH >> 4, tc = a.OW >> 4, PHo = a.OH >> 1, PWo = a.OW >> 1;
+  const int per_tile = 15 * 16;  // 15 border cells (j = 0 row: i 0..7, i = 0 column: j 1..7) x 16 c4
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)frames * tr * tc * per_tile) return;
+  const int c4 = (int)(idx & 15);
+  const int e = (int)((idx >> 4) % 15);
+  const int tl = (int)(idx / per_tile);
+  const int b = tl / (tr * tc), t2 = tl - b * tr * tc, th = t2 / tc, tw = t2 - th * tc;
+  const int j = e < 8 ? 0 : e - 7, i = e < 8 ? e : 0;
+  const int py = 8 * th + j, px = 8 * tw + i;
+  const bool up = j == 0 && th > 0, left = i == 0 && tw > 0;
+  if (!up && !left) return;
+  float* dst = a.y + ((size_t)(b * PHo + py) * PWo + px) * 64 + 4 * c4;
+  x6_f32x4 m = *reinterpret_cast<const x6_f32x4*>(dst);
+  auto merge = [&](int tile, int slot) {
+    const x6_f32x4 t = *reinterpret_cast<const x6_f32x4*>(a.part + ((size_t)tile * 17 + slot) * 64 + 4 * c4);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m[q] = fmaxf(m[q], t[q]);
+  };
+  if (up) merge(tl - tc, i);
+  if (left) merge(tl - 1, 9 + j);
+  if (up && left) merge(tl - tc - 1, 8);
+  *reinterpret_cast<x6_f32x4*>(dst) = m;
+}
+
 // ABL (timing ablations only, env SFA_STEM_ABL; results wrong): 1 = no epilogue, 2 = no MFMAs,
-// 4 = no patch fetch, 8 = first patch fetched after the weights are staged
+// 4 = no patch fetch, 8 = first patch fetched after the weights are staged,
+// 16 = border cells stored instead of atomicMax
 template <int ABL = 0>
 __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs a, int ntiles) {
   using namespace stem_patch;
@@ -206,7 +249,7 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs 
       __syncthreads();
     } else {
       const int tl = tile - b * tiles_per_frame, th = tl / tw_n;
-      stem_pool_epilogue(a, acc, reinterpret_cast<float*>(ST), b, th, tl - th * tw_n, wave, tid, ainv[0]);
+      stem_pool_epilogue<(ABL & 16) != 0>(a, acc, reinterpret_cast<float*>(ST), b, th, tl - th * tw_n, wave, tid, ainv[0]);
     }
   }
 }
@@ -217,7 +260,7 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
   const ConvSeg& g = a.seg[0];
   if (!a.wh || !a.winv || a.nseg != 1 || a.N != 64 || g.C != 4 || g.KH != 7 || g.KW != 7 || g.stride != 2 ||
       g.pad != 3 || a.Kpad < 196 || a.OH % 16 != 0 || a.OW % 16 != 0 || a.OH * 2 != g.H || a.OW * 2 != g.W ||
-      a.res || !a.relu) {
+      a.res || !a.relu || (a.part && a.part_floats < (size_t)a.M / 256 * 17 * 64)) {
     set_error("stem_patch: unsupported stem (C=%d k=%d OH=%d OW=%d)", g.C, g.KH, a.OH, a.OW);
     return SFA_E_UNSUPPORTED;
   }
@@ -244,7 +287,13 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
     case 4: hipLaunchKernelGGL(stem_patch_pool_kernel<4>, gd, bd, 0, st, a, ntiles); break;
     case 3: hipLaunchKernelGGL(stem_patch_pool_kernel<3>, gd, bd, 0, st, a, ntiles); break;
     case 8: hipLaunchKernelGGL(stem_patch_pool_kernel<8>, gd, bd, 0, st, a, ntiles); break;
+    case 16: hipLaunchKernelGGL(stem_patch_pool_kernel<16>, gd, bd, 0, st, a, ntiles); break;
     default: hipLaunchKernelGGL(stem_patch_pool_kernel<0>, gd, bd, 0, st, a, ntiles); break;
+  }
+  SFA_LAUNCH_CHECK();
+  if (a.part) {
+    const long long n = (long long)ntiles * 15 * 16;
+    hipLaunchKernelGGL(stem_pool_merge_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, frames);
   }
   SFA_LAUNCH_CHECK();
   return SFA_OK;
