@@ -138,7 +138,7 @@ class StepGraphs:
 
         def dec():
             _decoder(o["hm_cen"], o["cen_offset"], o["direction"], o["z_coor"], o["dim"], K=p.K,
-                     apply_sigmoid=True, out=p.dets, stream=_lib.stream_ptr(p.dev))
+                     apply_sigmoid=True, out=p.dets, stream=_lib.stream_ptr(p.dev), workspace=p.dec_ws)
 
         self.fns = [fwd, dec]
         self.graphs = None

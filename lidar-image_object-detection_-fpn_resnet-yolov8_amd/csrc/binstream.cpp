@@ -51,6 +51,10 @@ struct sfa_bin_stream {
   std::mutex mu;
   std::condition_variable cv;
   bool stop = false;
+  // sticky failure: once a hand-off to the device failed, every later next() returns it
+  // (the slot's state is unknown, so no batch is ever handed out from it again)
+  int failed = SFA_OK;
+  std::string failed_err;
   std::thread producer;
 };
 
@@ -215,6 +219,10 @@ extern "C" int sfa_bin_stream_next(sfa_bin_stream* s, float* points, int64_t cap
                                    int64_t* frame_offsets, int* n_frames, void* stream) {
   SFA_CHECK_ARG(s && points && frame_offsets && n_frames, "bin_stream_next: null argument");
   std::unique_lock<std::mutex> lk(s->mu);
+  if (s->failed != SFA_OK) {
+    set_error("%s", s->failed_err.c_str());
+    return s->failed;
+  }
   if (s->next_take >= s->nbatches) {
     *n_frames = 0;
     for (int i = 0; i <= s->batch; ++i) frame_offsets[i] = 0;
@@ -243,8 +251,24 @@ extern "C" int sfa_bin_stream_next(sfa_bin_stream* s, float* points, int64_t cap
   *n_frames = sl.nframes;
   if (s->pinned) {
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (npts > 0) SFA_HIP_TRY(hipMemcpyAsync(points, sl.host, (size_t)npts * 16, hipMemcpyHostToDevice, st));
-    SFA_HIP_TRY(hipEventRecord(sl.done, st));
+    hipError_t e = npts > 0 ? hipMemcpyAsync(points, sl.host, (size_t)npts * 16, hipMemcpyHostToDevice, st)
+                            : hipSuccess;
+    const bool copied = e == hipSuccess && npts > 0;
+    if (e == hipSuccess) e = hipEventRecord(sl.done, st);
+    if (e != hipSuccess) {
+      // the copy may be in flight with no event to wait on: drain the stream (best effort)
+      // before anyone may touch the slot, stop the producer and fail every later call
+      if (copied) (void)hipStreamSynchronize(st);
+      s->failed = SFA_E_HIP;
+      s->failed_err = std::string("bin_stream: batch ") + std::to_string(b) + ": device hand-off failed: " +
+                      hipGetErrorString(e);
+      s->stop = true;
+      sl.state = Slot::FREE;
+      lk.unlock();
+      s->cv.notify_all();
+      set_error("%s", s->failed_err.c_str());
+      return SFA_E_HIP;
+    }
     sl.state = Slot::IN_FLIGHT;  // the producer waits for `done` before refilling
   } else {
     memcpy(points, sl.host, (size_t)npts * 16);  // host destination (no device involved)

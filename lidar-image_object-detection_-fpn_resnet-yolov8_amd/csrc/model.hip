@@ -285,6 +285,9 @@ struct sfa_model {
   int fpn_commute = 7;  // fp16x3: bit f -> FPN conv f as up(W_a x) + W_b skip (env SFA_FPN_COMMUTE, mask)
   bool pool_fusion = true;  // fp16x3 stem + max-pool in one kernel (env SFA_STEM_POOL_FUSION=0: off)
   bool stem_patch = true;   // ... from LDS input patches (stem_patch_kernel.h; env SFA_STEM_PATCH=0: off)
+  // patch stem's tile-border pooled cells: owner tile + side buffer + merge pass (default), or
+  // (env SFA_STEM_PATCH_ATOMIC=1) atomicMax into the zeroed pooled buffer — same bits, A/B only
+  bool stem_atomic = false;
   // Side stream for the level-0 heads (they only need up_level2, so they overlap the rest
   // of the FPN and the level-1/2 heads); created with the model on the current device,
   // used only when the forward's stream is on that device.
@@ -434,6 +437,7 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   m->math = SFA_MATH_FP16X3;
   if (const char* e = getenv("SFA_STEM_POOL_FUSION")) m->pool_fusion = strcmp(e, "0") != 0;
   if (const char* e = getenv("SFA_STEM_PATCH")) m->stem_patch = strcmp(e, "0") != 0;
+  if (const char* e = getenv("SFA_STEM_PATCH_ATOMIC")) m->stem_atomic = strcmp(e, "0") != 0;
   if (const char* e = getenv("SFA_FPN_COMMUTE")) m->fpn_commute = atoi(e) & 7;
   if (hipGetDevice(&m->device) != hipSuccess ||
       hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking) != hipSuccess ||
@@ -626,18 +630,25 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   }
   const int H2 = H / 2, W2 = W / 2;
   // stem conv7x7/s2/p3 + BN + ReLU   (fpn_resnet.py:179-181)
-  // fp16x3 with an 8x16-tileable stem output: the max-pool (:182) runs in the stem's epilogue
-  // (pooled buffer zeroed first: its tile-border cells are combined with atomicMax)
+  // fp16x3 with an 8x16-tileable stem output: the max-pool (:182) runs in the stem's epilogue.
+  // Patch stem (default): every pooled cell has one owner tile, the neighbours' parts of the
+  // tile-border cells go through a side buffer and a merge pass (no memset, no atomics).
+  // Implicit-GEMM stem (SFA_STEM_PATCH=0) and the patch stem's A/B form
+  // (SFA_STEM_PATCH_ATOMIC=1): pooled buffer zeroed, border cells combined with atomicMax.
   const bool pool_fused = h3 && m->pool_fusion && H2 % 8 == 0 && W2 % 16 == 0;
   {
     ConvArgs a = conv_args(wb, p.stem, B, H2, W2, pool_fused ? F(bf.p0) : F(bf.s0), nullptr, 1);
     a.seg[0] = seg(xin, B, H, W, 4, 7, 2, 3);
     io(a, AM_INPUT, -1, AM_STEM);
     if (pool_fused && m->stem_patch && H2 % 16 == 0 && W2 % 16 == 0) {
-      // every pooled cell has one owner tile; the tile-border parts of the neighbours go
-      // through the (here unused) unfused stem buffer and a merge pass: no memset, no atomics
-      a.part = F(bf.s0);
-      a.part_floats = (size_t)B * H2 * W2 * 64;
+      if (m->stem_atomic) {
+        a.part = nullptr;
+        a.part_floats = 0;
+        SFA_HIP_TRY(hipMemsetAsync(F(bf.p0), 0, (size_t)B * (H2 / 2) * (W2 / 2) * 64 * sizeof(float), st));
+      } else {
+        a.part = F(bf.s0);  // the (here unused) unfused stem buffer
+        a.part_floats = (size_t)B * H2 * W2 * 64;
+      }
       SFA_RC(launch_stem_patch(a, st));
     } else if (pool_fused) {
       SFA_HIP_TRY(hipMemsetAsync(F(bf.p0), 0, (size_t)B * (H2 / 2) * (W2 / 2) * 64 * sizeof(float), st));
@@ -793,6 +804,12 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     fork_lock.lock();
     SFA_HIP_TRY(hipEventRecord(m->fork, st));
     SFA_HIP_TRY(hipStreamWaitEvent(m->side, m->fork, 0));
+  }
+  // Everything between the fork and the join: any failure inside returns from this lambda
+  // only, so the side stream is still joined below (a graph capture stays valid, no work is
+  // left orphaned on the side stream).
+  auto forked = [&]() -> int {
+  if (overlap) {
     SFA_RC(launch_head(0, m->side));
   } else {
     SFA_RC(launch_head(0, st));
@@ -831,11 +848,17 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     SFA_HIP_TRY(hipEventRecord(m->mid, st));
     SFA_HIP_TRY(hipStreamWaitEvent(m->side, m->mid, 0));
     SFA_RC(launch_head(2, m->side));
-    SFA_HIP_TRY(hipEventRecord(m->join, m->side));
   }
   SFA_RC(launch_head(1, st));
   if (!overlap) SFA_RC(launch_head(2, st));
-  if (overlap) SFA_HIP_TRY(hipStreamWaitEvent(st, m->join, 0));
+  return SFA_OK;
+  };
+  const int frc = forked();
+  if (overlap) {  // the join, on success and on failure alike
+    SFA_HIP_TRY(hipEventRecord(m->join, m->side));
+    SFA_HIP_TRY(hipStreamWaitEvent(st, m->join, 0));
+  }
+  SFA_RC(frc);
   // apply_kfpn (fpn_resnet.py:248-254)
   KfpnOut ko;
   memset(&ko, 0, sizeof ko);

@@ -35,9 +35,14 @@ constexpr int LDS_BYTES = W_BYTES + 2 * PATCH_TERM + T_BYTES;  // 151,600 B: one
 // the frame's max recorded, then the 9 x 9 pooled cells whose 3 x 3/s2 window touches the
 // tile (pooled rows 8 th .. 8 th + 8, cols 8 tw .. 8 tw + 8): each thread takes one cell and
 // four channels, its window's nine float4 reads unrolled (indices clamped to the tile: a
-// repeated element does not change a max). Cells with one writer (j, i in 1..7) are stored,
-// the tile-border cells shared with a neighbour combined by atomicMax on the f32 bits
-// (values >= +0) into the zeroed pooled buffer — the same rule as h3_pool_epilogue.
+// repeated element does not change a max).
+// Default (a.part != null, no memset, no atomics): the tile stores the cells it owns (j, i <= 7:
+// the cell's conv pixel (2 py, 2 px) lies in this tile) and writes its parts of the lower /
+// right neighbours' cells (row j = 8, column i = 8) to its 17 side-buffer slots;
+// stem_pool_merge_kernel folds those in. A/B form (a.part == null, SFA_STEM_PATCH_ATOMIC=1):
+// cells with one writer (j, i in 1..7) are stored, the tile-border cells combined by
+// atomicMax on the f32 bits (values >= +0) into the zeroed pooled buffer, as
+// h3_pool_epilogue does. NOATOM (ablation ABL 16) applies to the A/B form only.
 template <bool NOATOM = false>
 __device__ __forceinline__ void stem_pool_epilogue(const ConvArgs& a, x6_f32x16 (&acc)[1][2], float* T, int b,
                                                    int th, int tw, int wave, int tid, float ainv) {
@@ -137,7 +142,7 @@ __global__ void __launch_bounds__(256) stem_pool_merge_kernel(const ConvArgs a, 
 
 // ABL (timing ablations only, env SFA_STEM_ABL; results wrong): 1 = no epilogue, 2 = no MFMAs,
 // 4 = no patch fetch, 8 = first patch fetched after the weights are staged,
-// 16 = border cells stored instead of atomicMax
+// 16 = border cells stored instead of atomicMax (only with a.part == null: the atomic A/B form)
 template <int ABL = 0>
 __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs a, int ntiles) {
   using namespace stem_patch;

@@ -93,12 +93,19 @@ class KfpnEngine:
     def workspace_bytes(self, B, H, W) -> int:
         return int(lib().sfa_forward_workspace_size(self._h, B, H, W))
 
-    def workspace(self, B, H, W) -> torch.Tensor:
-        key = (B, H, W)
-        ws = self._ws.get(key)
-        if ws is None:
-            ws = torch.empty(self.workspace_bytes(B, H, W), dtype=torch.uint8, device=self.device)
-            self._ws = {key: ws}  # keep only the latest shape resident
+    def workspace(self, B, H, W, stream: int = None) -> torch.Tensor:
+        """The forward workspace (activations + fp16x3 max slots) for one stream: forwards on
+        different streams never share one (two concurrent forwards on one stream are ordered
+        by it). One shape per stream stays resident; replacing it first waits for the device,
+        so a forward still running on the old buffer cannot see it reused."""
+        sk = int(stream) if stream is not None else _lib.stream_ptr(self.device)
+        cur = self._ws.get(sk)
+        if cur is not None and cur[0] == (B, H, W):
+            return cur[1]
+        if cur is not None:
+            torch.cuda.synchronize(self.device)
+        ws = torch.empty(self.workspace_bytes(B, H, W), dtype=torch.uint8, device=self.device)
+        self._ws[sk] = ((B, H, W), ws)
         return ws
 
     def alloc_outputs(self, B, H, W):
@@ -115,11 +122,11 @@ class KfpnEngine:
             B, H, W, C = x.shape
             if C != 4:
                 raise ValueError(f"expected (B, H, W, 4) input, got {tuple(x.shape)}")
-        ws = workspace if workspace is not None else self.workspace(B, H, W)
+        sp = stream if stream is not None else _lib.stream_ptr(self.device)
+        ws = workspace if workspace is not None else self.workspace(B, H, W, sp)
         ptrs = (ctypes.c_void_p * len(self.heads))(*[outs[n].data_ptr() for n, _ in self.heads])
         check(lib().sfa_model_forward(self._h, x.data_ptr(), in_layout, B, H, W, ptrs, ws.data_ptr(),
-                                      ws.numel(), stream if stream is not None else
-                                      _lib.stream_ptr(self.device)), "sfa_model_forward")
+                                      ws.numel(), sp), "sfa_model_forward")
         return outs
 
     def debug_views(self, ws: torch.Tensor, B, H, W) -> dict:
@@ -243,22 +250,27 @@ def sigmoid_clamp_(x: torch.Tensor) -> torch.Tensor:
 
 
 class Decoder:
-    """sfa_decode with a cached workspace."""
+    """sfa_decode with a workspace cached per (device, stream, shape): decodes on different
+    streams never share scratch."""
 
     def __init__(self):
         self._ws = {}
 
-    def workspace(self, device, B, C, K):
-        key = (str(device), B, C, K)
+    @staticmethod
+    def workspace_bytes(B, C, K) -> int:
+        return int(lib().sfa_decode_workspace_size(B, C, K))
+
+    def workspace(self, device, B, C, K, stream: int = None):
+        sk = int(stream) if stream is not None else _lib.stream_ptr(device)
+        key = (str(device), sk, B, C, K)
         ws = self._ws.get(key)
         if ws is None:
-            ws = torch.empty(int(lib().sfa_decode_workspace_size(B, C, K)), dtype=torch.uint8,
-                             device=device)
+            ws = torch.empty(self.workspace_bytes(B, C, K), dtype=torch.uint8, device=device)
             self._ws[key] = ws
         return ws
 
     def __call__(self, hm, off, dirn, z, dim, K=40, apply_sigmoid=False, out=None,
-                 stream: int = None):
+                 stream: int = None, workspace: torch.Tensor = None):
         hm = _require_gpu_tensor(hm, "decode")
         dirn, z, dim = (_require_gpu_tensor(t, "decode") for t in (dirn, z, dim))
         if off is not None:
@@ -269,11 +281,14 @@ class Decoder:
                 raise ValueError(f"decode: map shape {tuple(t.shape)} != {(B, c, H, W)}")
         if out is None:
             out = torch.empty((B, K, 10), dtype=torch.float32, device=hm.device)
-        ws = self.workspace(hm.device, B, C, K)
+        sp = stream if stream is not None else _lib.stream_ptr(hm.device)
+        ws = workspace if workspace is not None else self.workspace(hm.device, B, C, K, sp)
+        if ws.numel() < self.workspace_bytes(B, C, K):
+            raise ValueError("decode: workspace too small")
         check(lib().sfa_decode(hm.data_ptr(), off.data_ptr() if off is not None else None,
                                dirn.data_ptr(), z.data_ptr(), dim.data_ptr(), B, C, H, W, int(K),
                                1 if apply_sigmoid else 0, out.data_ptr(), ws.data_ptr(), ws.numel(),
-                               stream if stream is not None else _lib.stream_ptr(hm.device)),
+                               sp),
               "sfa_decode")
         return out
 
@@ -311,10 +326,14 @@ class DetectorPipeline:
         nmap = 2 * batch if self.two_sided else batch
         self.nmap = nmap
         with torch.cuda.device(self.dev):
-            self.ws = engine.workspace(nmap, height, width)
+            # the pipeline's own workspace (it is replayed on streams of the caller's choosing,
+            # so it must not be the engine's per-stream cache entry)
+            self.ws = torch.empty(engine.workspace_bytes(nmap, height, width), dtype=torch.uint8,
+                                  device=self.dev)
             self.outs = engine.alloc_outputs(nmap, height, width)
             self.dets = torch.empty((nmap, K, 10), dtype=torch.float32, device=self.dev)
-            self.dec_ws = _decoder.workspace(self.dev, nmap, dict(engine.heads)["hm_cen"], K)
+            self.dec_ws = torch.empty(Decoder.workspace_bytes(nmap, dict(engine.heads)["hm_cen"], K),
+                                      dtype=torch.uint8, device=self.dev)
             if with_bev:
                 if (height, width) != (608, 608):
                     raise ValueError("the BEV grid is 608x608 (config/kitti_config.py:45-46)")
@@ -365,7 +384,7 @@ class DetectorPipeline:
             self.engine.forward_into(self.x, self.outs, _lib.IN_NCHW3, self.ws, st)
         o = self.outs
         _decoder(o["hm_cen"], o["cen_offset"], o["direction"], o["z_coor"], o["dim"], K=self.K,
-                 apply_sigmoid=True, out=self.dets, stream=st)
+                 apply_sigmoid=True, out=self.dets, stream=st, workspace=self.dec_ws)
         return self.dets
 
     def capture(self):

@@ -192,6 +192,24 @@ def test_stem_pool_fusion_bit_exact(golden, gpu, monkeypatch):
         np.testing.assert_array_equal(outs[0][h], outs[1][h])
 
 
+def test_stem_patch_side_buffer_bit_exact(golden, gpu, monkeypatch):
+    """Patch stem: tile-border pooled cells through the owner tile + side buffer +
+    stem_pool_merge_kernel (default) == atomicMax into the zeroed pooled buffer
+    (SFA_STEM_PATCH_ATOMIC=1), bit for bit over the whole forward. 160x192 -> an 80x96 conv
+    output = 5x6 tiles of 16x16, so the up, left and up-left (corner) merges all run."""
+    x = torch.from_numpy(synthetic.synthetic_bev(3, 160, 192, seed=23)).to(gpu)
+    outs = []
+    monkeypatch.setenv("SFA_STEM_PATCH", "1")
+    for flag in ("0", "1"):
+        monkeypatch.setenv("SFA_STEM_PATCH_ATOMIC", flag)
+        model = make_model(golden, gpu)  # the flag is read when the native model is created
+        model._engine(gpu).set_math(_math("fp16x3"))
+        with torch.no_grad():
+            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(outs[0][h], outs[1][h])
+
+
 @pytest.mark.parametrize("hw", [(160, 192), (608, 608)])
 def test_stem_patch_matches_gather_stem(golden, gpu, monkeypatch, hw):
     """fp16x3 stem + pool from LDS input patches (stem_patch_kernel.h: K laid out with kw
