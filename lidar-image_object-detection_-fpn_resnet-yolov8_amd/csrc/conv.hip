@@ -6,6 +6,7 @@
 #include "conv_x6_kernel.h"
 #include "conv_h3_kernel.h"
 #include "conv_h3s_kernel.h"
+#include "conv_r3_kernel.h"
 #include "stem_patch_kernel.h"
 
 namespace sfa {
@@ -51,6 +52,12 @@ static bool strip_ok(const ConvArgs& a) {
 //    kept selectable (SFA_TUNE bit 2), not the default;
 //  * the rest (stride-2 convs, 2-segment convs, 1x1 FPN convs, the stem): conv_h3_kernel,
 //    16x16x32 for the 64-wide ones, 32x32x16 for the 128..512-wide ones, BK 16 for the stem;
+//  * round 2: conv_r3_kernel (conv_r3_kernel.h: A fragments loaded straight into registers,
+//    only W through LDS, W DMA spread over the column blocks) for the heads (-7..8 % vs
+//    conv_h3_kernel), the 128-wide stride-1 layer2 convs (-10 % vs the strip kernel) and every
+//    128..512-wide conv the strip kernel cannot take (stride 2, conv + downsample segments,
+//    K-sliced FPN convs: -3..25 %; profiles/r02_convbench_*.txt); SFA_TUNE bits 4 / 16 / 8
+//    return those three groups to the round-1 kernels for same-box A/B;
 //  * split-K 2 for the 512-wide (layer4) convs, whose 184 tiles cannot fill 256 CUs (-13..16 %);
 //    picked from the width only, so a frame's arithmetic never depends on the batch.
 // conv_x6g_kernel<..., PREC 1> tiles as the fallback.
@@ -71,7 +78,8 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   const bool strip = strip_ok(a) && !sliced;
   if (epilogue == EPI_HEAD) {
     if (a.N == 320) {
-      rc = launch_conv_h3_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2, 1>(a, st);
+      if (!(tune_flags() & 4)) rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, 260>(a, st);
+      if (!ok(rc)) rc = launch_conv_h3_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2, 1>(a, st);
       if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 320, 32, EPI_HEAD, 1, 16, 3, 0, 320, 1>(a, st);
     }
     if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_HEAD, 1, 16, 3, 0, 64, 1>(a, st);
@@ -91,8 +99,13 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     ConvArgs b = a;
     b.ksplit = a.part && a.N >= 512 && !sliced && a.bias ? 2 : 1;
     if (strip) {
-      if (tune_flags() & 2) rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3>(b, st);
-      else rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
+      if (a.N == 128 && a.M >= 50000 && !(tune_flags() & 16))
+        rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, 256>(b, st);
+      else if (tune_flags() & 2)
+        rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3>(b, st);
+      if (!ok(rc)) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
+    } else if (!(tune_flags() & 8)) {  // stride-2 / two-segment / K-sliced: A from registers
+      rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, 256>(b, st);
     }
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
     if (!ok(rc) && b.ksplit > 1) {  // K not divisible into the slices: no split

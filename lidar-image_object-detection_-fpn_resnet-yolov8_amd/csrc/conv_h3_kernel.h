@@ -32,7 +32,7 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 // x6_epilogue<..., PREC = 1>: scale back by 1/s of the row's frame and winv[n], bias,
 // residual, ReLU, store, per-frame max |y|; EPI_HEAD stages ReLU(conv3x3 + b) of each head
 // in LDS and applies its 1x1 conv, channel-planar out.
-template <int BM, int BN, int WM, int WN, int TM, int TN, int NT, int EPI>
+template <int BM, int BN, int WM, int WN, int TM, int TN, int NT, int EPI, bool RES_UP = true>
 __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
                                               int m0, int n0, int nt, int wave, int wn, int tid,
                                               const float (&ainv)[TM]) {
@@ -57,7 +57,7 @@ __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[
             rv[mi][ni][v] = a.res[(size_t)m * a.N + n0 + wn * WN + ni * 16 + c16];
           }
     }
-    if (a.res_up) {
+    if (RES_UP && a.res_up) {
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni)
 #pragma unroll
@@ -80,7 +80,7 @@ __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[
           const int m = m0 + wave * WM + mi * 16 + 4 * g + v;
           if (m < M) {
             float val = acc[mi][ni][v] * rinv[mi][v] * cs + bn;
-            if (a.res || a.res_up) val += rv[mi][ni][v];
+            if (a.res || (RES_UP && a.res_up)) val += rv[mi][ni][v];
             if (a.relu) val = fmaxf(val, 0.f);
             a.y[(size_t)m * a.N + n] = val;
             if (a.amax_out) am.add(a.amax_out, m, val);

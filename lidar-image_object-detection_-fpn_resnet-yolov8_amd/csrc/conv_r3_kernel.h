@@ -1,0 +1,399 @@
+// Implicit-GEMM convolution, fp16x3 arithmetic, A operand in REGISTERS (gfx950 / CDNA4).
+//
+// Same GEMM view, operand split, scales and epilogues as conv_h3_kernel<..., MF = 1>
+// (conv_h3_kernel.h): C[M][N] = A[M][K] * W[N][K]^T over NHWC, products hi*hi + hi*lo + lo*hi
+// on v_mfma_f32_16x16x32_f16 with f32 accumulation, BK = 32 (one MFMA k-step per K-tile).
+// What differs is where A lives. The waves are stacked along M (each wave owns WM rows x all
+// BN columns), so no wave ever reads another wave's A rows: each lane loads its own fragment
+// (row l & 15 of each 16-row sub-tile, f32 k = 8 (l >> 4) .. +7 = 32 contiguous bytes of one
+// input pixel) straight into VGPRs with two buffer loads, one K-tile ahead, and splits it
+// into the fp16 terms at the top of the K-tile. Only the weights (shared by all waves) go
+// through LDS, by LDS-DMA into an NSTAGE-deep ring. Compared with staging A through LDS:
+//  * the per-tile A DMA pieces, their LDS writes and the A fragment ds_reads are gone;
+//  * after a K-tile's barrier a wave has nothing to wait for: its A fragment arrived during
+//    the previous tile and (NSTAGE 3) the first two W fragment blocks were read before the
+//    barrier, so the MFMAs restart at once instead of behind DMA issue + ds_read + split;
+//  * the W DMA of tile kt + NSTAGE - 1 and the A loads of tile kt + 1 are issued between the
+//    MFMAs of column blocks 0 and 1 (pinned by sched_barrier), not in a burst after the barrier.
+// Synchronisation per K-tile kt (tile kt in stage kt % NSTAGE):
+//   split A(kt) (hipcc waits for the A loads: vmcnt(0), nothing else is outstanding yet)
+//   block 0: W DMA of tile kt + NSTAGE - 1 into stage (kt - 1) % NSTAGE (last read in tile
+//            kt - 1, before the previous barrier); block 1: A loads of tile kt + 1
+//   blocks ni: W fragments read two blocks ahead; with NSTAGE 3 blocks TN, TN + 1 are tile
+//            kt + 1's first two, from its stage (landed and published by the previous barrier)
+//   s_waitcnt vmcnt(2 TM) (this wave's W DMAs have landed, its A loads may still fly); s_barrier
+// LDS image of W (per term, rows of 64 B, 16-B chunk q of row R stored at q ^ swzB(R)) as in
+// conv_h3_kernel's 16x16x32 form: conflict-free ds_read_b128 for its lane groups.
+#pragma once
+
+#include "conv_h3_kernel.h"
+
+namespace sfa {
+
+typedef unsigned r3_u32x4 __attribute__((ext_vector_type(4)));
+
+// ABL (tools/convbench variants): 1 = no W DMA in the K loop (ablation), 4 = s_setprio 1 for the
+// second half of the waves, 8 = do not pin the DMA / A-load placement (compiler scheduling; the
+// end-of-tile wait is then vmcnt(0), since the W DMAs are no longer known to precede the A loads),
+// 16 = split the next tile's A during this tile's MFMAs (hf / hn double buffer, +16 VGPRs),
+// 32 = pure MFMA stream (no loads, split, W reads or barriers in the K loop: the ceiling),
+// 64 = no split in the K loop (A loads kept live), 128 = no barrier in the K loop (ablations),
+// 256 = spread the W DMA: A loads at block 0, then one W piece per block from block 2, the two
+// waves of a SIMD (w, w + NW/2) on alternate blocks, so no SIMD issues two DMA bursts at once,
+// 512 = staggered split: waves w < NW/2 split the next tile's A at block SPLIT_AT (into hn),
+// the others at the top of their tile, so after a barrier one wave of each SIMD issues MFMAs
+// while its partner splits.
+template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int NSEG, int ABL = 0>
+__global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const ConvArgs a) {
+  static_assert(NSTAGE == 2 || NSTAGE == 3, "W ring depth");
+  static_assert(NSEG == 1 || NSEG == 2, "segments");
+  static_assert(EPI == EPI_STD || EPI == EPI_HEAD, "epilogue");
+  constexpr int NW = BM / WM, NT = NW * 64;
+  constexpr int TM = WM / 16, TN = BN / 16;
+  constexpr int BK = 32, BROW = BK * 2;  // W row bytes per term
+  constexpr int TERM_B = BN * BROW, STAGE = 2 * TERM_B;
+  constexpr int ND_BT = TERM_B / 1024, ND_B = 2 * ND_BT;  // 1-KiB DMA pieces (16 rows each)
+  constexpr int NB = (ND_B + NW - 1) / NW;
+  constexpr int NB_REM = ND_B % NW;  // if != 0: waves < NB_REM issue NB pieces, the rest NB - 1
+  static_assert(BM % WM == 0 && WM % 16 == 0 && BN % 16 == 0 && TERM_B % 1024 == 0, "tile");
+  static_assert(TN >= 2, "two W blocks in flight");
+  constexpr int EPI_BYTES = EPI == EPI_HEAD ? BM * 65 * 4 + (BN / 64) * 1024 : 2 * NW * 4;
+  constexpr int LDS_BYTES = NSTAGE * STAGE > EPI_BYTES ? NSTAGE * STAGE : EPI_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
+
+  auto swzB = [](int R) { return ((R >> 2) & 3) ^ ((((R & 15) + 4) >> 3) & 1); };
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c16 = lane & 15, g = lane >> 4;
+  const int n_tiles = a.N / BN;
+  const int m_tiles = (a.M + BM - 1) / BM;
+  const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
+  int lbid = xcd_remap(blockIdx.x, gridDim.x);
+  const int kz = lbid / (m_tiles * n_tiles);  // split-K slice of this block
+  lbid -= kz * (m_tiles * n_tiles);
+  const int mt = lbid / n_tiles, nt = lbid - mt * n_tiles;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int M = a.M;
+
+  // ---- A: this lane's rows (one per 16-row sub-tile), gather origins per segment ----
+  int r_pix[NSEG][TM], r_ihw[NSEG][TM];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+    const int m = m0 + wave * WM + mi * 16 + c16;
+    const bool ok = m < M;
+    const int mm = ok ? m : 0;
+    const int ow = mm % a.OW, t = mm / a.OW;
+    const int oh = t % a.OH, b = t / a.OH;
+#pragma unroll
+    for (int sg = 0; sg < NSEG; ++sg) {
+      const ConvSeg& sgm = a.seg[sg];
+      const int ih = ok ? oh * sgm.stride - sgm.pad : -16384;
+      const int iw = ow * sgm.stride - sgm.pad;
+      r_pix[sg][mi] = (b * sgm.H + ih) * sgm.W + iw;
+      r_ihw[sg][mi] = (ih << 16) | (iw & 0xffff);
+    }
+  }
+  const __amdgpu_buffer_rsrc_t rs0 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.seg[0].x), (short)0, (int)a.seg[0].bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs1 = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.seg[NSEG - 1].x), (short)0, (int)a.seg[NSEG - 1].bytes, 0x00020000);
+
+  // ---- W DMA slots: pieces e = wave + NW * j (term e / ND_BT, rows (e % ND_BT) * 16 + lane / 4) ----
+  const int wst = a.wstride ? a.wstride : a.Kpad;  // row stride of the fp16 terms
+  const unsigned term_bytes = (unsigned)a.N * (unsigned)wst * 2u;
+  const __amdgpu_buffer_rsrc_t rsw =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.wh), (short)0, (int)(2 * term_bytes), 0x00020000);
+  // row R = 16 (e % ND_BT) + lane / 4 of piece e has swzB(R) = swzB(lane / 4), so the lane part
+  // of the source offset is the same for every piece and the piece part is wave-uniform
+  // (one VGPR for all NB pieces; a non-constant soffset operand of the LDS-DMA builtin makes
+  // hipcc's host pass drop the kernel stub, so the uniform part is added to the VGPR offset)
+  const int wlane = (((n0 + lane / 4) * wst + a.wk0 + 8 * ((lane % 4) ^ swzB(lane / 4))) << 1);
+  int boff_s[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const int e = wave + NW * j < ND_B ? wave + NW * j : ND_B - 1;
+    boff_s[j] = (int)((e / ND_BT) * term_bytes) + (e % ND_BT) * 16 * wst * 2;  // uniform: wave, j, args
+  }
+
+  // fp16x3 scale of the frame of this lane's A row in each 16-row sub-tile
+  float as[TM];  // 1 / as (exact: powers of two) is recomputed for the epilogue
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+    const int m = min(m0 + wave * WM + mi * 16 + c16, M - 1);
+    float sinv;
+    as[mi] = amax_frame_scale(a.amax_in, NSEG, m / (a.OH * a.OW), sinv);
+  }
+
+  r3_u32x4 raw[TM][2];  // A fragment of the next K-tile (f32 bits)
+  auto load_a_seg = [&](auto sgc, const __amdgpu_buffer_rsrc_t rs, int kl) {
+    constexpr int SG = decltype(sgc)::value;
+    const ConvSeg& sgm = a.seg[SG];
+    const int kk = kl + 8 * g;
+    const int tap = kk >> sgm.logC;
+    const int c = kk & (sgm.C - 1);
+    const int kh = (tap * sgm.kdiv_mul) >> sgm.kdiv_sh;
+    const int kw = tap - kh * sgm.KW;
+    const bool tap_ok = tap < sgm.taps;
+    const int toff = kh * sgm.W + kw;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int ih = r_ihw[SG][mi] >> 16;
+      const int iw = (int)(short)(r_ihw[SG][mi] & 0xffff);
+      const bool ok = tap_ok & ((unsigned)(ih + kh) < (unsigned)sgm.H) & ((unsigned)(iw + kw) < (unsigned)sgm.W);
+      const unsigned off = ok ? (unsigned)((((r_pix[SG][mi] + toff) << sgm.logC) + c) << 2) : 0x80000000u;
+      raw[mi][0] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+      raw[mi][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16u, 0, 0);
+    }
+  };
+  auto load_a = [&](int kt) {
+    const int k0 = kt * BK;
+    if constexpr (NSEG == 2) {
+      if (k0 >= a.kseg1)
+        load_a_seg(std::integral_constant<int, 1>(), rs1, k0 - a.kseg1);
+      else
+        load_a_seg(std::integral_constant<int, 0>(), rs0, k0);
+    } else {
+      load_a_seg(std::integral_constant<int, 0>(), rs0, k0);
+    }
+  };
+  auto load_w_piece = [&](int j, int kt, unsigned char* S) {
+    if (NB_REM == 0 || j < NB - 1 || wave < NB_REM)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsw, (__attribute__((address_space(3))) void*)(S + (wave + NW * j) * 1024), 16,
+          (unsigned)(wlane + boff_s[j] + 2 * kt * BK), 0, 0, 0);
+  };
+  auto load_w = [&](int kt, unsigned char* S) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      if (NB_REM == 0 || j < NB - 1 || wave < NB_REM)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsw, (__attribute__((address_space(3))) void*)(S + (wave + NW * j) * 1024), 16,
+            (unsigned)(wlane + boff_s[j] + 2 * k0), 0, 0, 0);
+    }
+  };
+  f16x8_t hf[2][TM], hn[2][TM];  // split A of this K-tile / of the next (ABL 16)
+  auto split_a = [&](f16x8_t (&h)[2][TM]) {
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      f16x4_t t0, t1, u0, u1;
+      split2h(__builtin_bit_cast(x6_f32x4, raw[mi][0]), as[mi], t0, t1);
+      split2h(__builtin_bit_cast(x6_f32x4, raw[mi][1]), as[mi], u0, u1);
+      h[0][mi] = __builtin_shufflevector(t0, u0, 0, 1, 2, 3, 4, 5, 6, 7);
+      h[1][mi] = __builtin_shufflevector(t1, u1, 0, 1, 2, 3, 4, 5, 6, 7);
+    }
+  };
+  // ABL 16: the next tile's A is split between the MFMAs of column block SPLIT_AT (into hn)
+  // instead of at the top of its own tile, so no split VALU sits between barrier and MFMAs
+  constexpr int SPLIT_AT = TN > 6 ? TN - 4 : TN - 1;
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[mi][ni][v] = 0.f;
+
+  const int bfo = c16 * BROW + ((g ^ swzB(c16)) << 4);  // this lane's W fragment in a block
+  f16x8_t bq[3][2];  // W fragment ring: block p in slot p % 3
+  auto read_b = [&](const unsigned char* S, int ni, f16x8_t (&dst)[2]) {
+    dst[0] = *reinterpret_cast<const f16x8_t*>(S + bfo + ni * 16 * BROW);
+    dst[1] = *reinterpret_cast<const f16x8_t*>(S + TERM_B + bfo + ni * 16 * BROW);
+  };
+
+  const int nk = a.Kpad / BK / nsplit;  // this block's K-tiles: kt0 .. kt0 + nk - 1
+  const int kt0 = kz * nk;
+  constexpr int NA_OPS = 2 * TM;  // A loads per K-tile (issued after the tile's W DMA)
+  // prologue: W tiles 0 .. NSTAGE-2, A tile 0; this wave's W landed, then everyone's
+#pragma unroll
+  for (int p = 0; p < NSTAGE - 1; ++p)
+    if (p < nk) load_w(kt0 + p, smem + p * STAGE);
+  load_a(kt0);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA_OPS) : "memory");
+  __builtin_amdgcn_s_barrier();
+  if constexpr ((ABL & 48) != 0) split_a(hf);
+  if constexpr ((ABL & 512) != 0) {
+    if (wave >= NW / 2 ? 0 : 1) split_a(hf);
+  }
+  if constexpr (NSTAGE == 3) {
+    read_b(smem, 0, bq[0]);
+    read_b(smem, 1, bq[1]);
+  }
+  if constexpr ((ABL & 4) != 0) {
+    if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+  }
+  const int wave_half = wave >= NW / 2 ? 1 : 0;  // SIMD partners: waves w and w + NW / 2
+  int st_cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const unsigned char* S = smem + st_cur * STAGE;
+    const int st_nx = st_cur + 1 == NSTAGE ? 0 : st_cur + 1;
+    const int st_w = st_cur == 0 ? NSTAGE - 1 : st_cur - 1;  // stage of tile kt + NSTAGE - 1
+    const bool more_w = (ABL & 32) == 0 && kt + NSTAGE - 1 < nk, more_a = (ABL & 32) == 0 && kt + 1 < nk;
+    if constexpr ((ABL & 512) != 0) {
+      if (wave_half) split_a(hf);
+    } else if constexpr ((ABL & 48) == 0) {
+      split_a(hf);
+    }
+    // keep the W DMA below the split: hipcc's wait for the A loads would otherwise also wait
+    // for DMAs issued just before it (it counts the conditional DMA path conservatively)
+    if constexpr ((ABL & 8) == 0) __builtin_amdgcn_sched_barrier(0);
+    if constexpr (NSTAGE == 2) {
+      read_b(S, 0, bq[0]);
+      read_b(S, 1, bq[1]);
+    }
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      if constexpr ((ABL & 256) == 0) {
+        if (ni == 0 && more_w && !(ABL & 1)) load_w(kt0 + kt + NSTAGE - 1, smem + st_w * STAGE);
+        if (ni == (TN > 2 ? 1 : 0) && more_a) load_a(kt0 + kt + 1);
+      } else {
+        // PPB pieces per issuing block; blocks 2, 4, .. for one half of the waves, 3, 5, .. for the other
+        constexpr int SLOTS = (TN - 2) / 2 >= 1 ? (TN - 2) / 2 : 1;
+        constexpr int PPB = (NB + SLOTS - 1) / SLOTS;
+        static_assert(TN >= 4, "spread DMA needs 4 column blocks");
+        if (ni == 0 && more_a) load_a(kt0 + kt + 1);
+        if (ni >= 2 && ((ni - 2) >> 1) * PPB < NB && more_w && !(ABL & 1) && wave_half == (ni & 1)) {
+#pragma unroll
+          for (int jj = 0; jj < PPB; ++jj) {
+            const int j = ((ni - 2) >> 1) * PPB + jj;
+            if (j < NB) load_w_piece(j, kt0 + kt + NSTAGE - 1, smem + st_w * STAGE);
+          }
+        }
+      }
+      const int p = ni + 2;
+      if ((ABL & 32) != 0) {
+        asm volatile("" : "+v"(bq[p % 3][0]), "+v"(bq[p % 3][1]));
+      } else if (p < TN)
+        read_b(S, p, bq[p % 3]);
+      else if (NSTAGE == 3 && more_a)
+        read_b(smem + st_nx * STAGE, p - TN, bq[p % 3]);
+      const f16x8_t c0 = bq[ni % 3][0], c1 = bq[ni % 3][1];
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        f32x4_t cc = acc[mi][ni];
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[1][mi], c0, cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c1, cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c0, cc, 0, 0, 0);
+        acc[mi][ni] = cc;
+      }
+      if constexpr ((ABL & 16) != 0 && (ABL & 64) == 0) {
+        if (ni == SPLIT_AT && more_a) split_a(hn);
+      }
+      if constexpr ((ABL & 512) != 0) {
+        if (ni == SPLIT_AT && more_a && !wave_half) split_a(hn);
+      }
+      if constexpr ((ABL & 64) != 0) {
+        if (ni == SPLIT_AT && more_a) {
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi) asm volatile("" ::"v"(raw[mi][0]), "v"(raw[mi][1]));
+        }
+      }
+      if constexpr ((ABL & 8) == 0) __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr ((ABL & 16) != 0 && (ABL & 64) == 0) {
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        hf[0][mi] = hn[0][mi];
+        hf[1][mi] = hn[1][mi];
+      }
+    }
+    if constexpr ((ABL & 512) != 0) {
+      if (!wave_half) {
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) {
+          hf[0][mi] = hn[0][mi];
+          hf[1][mi] = hn[1][mi];
+        }
+      }
+    }
+    if constexpr (NSTAGE == 3) {  // next tile's blocks 0, 1 into slots 0, 1
+      const f16x8_t n0a = bq[TN % 3][0], n0b = bq[TN % 3][1];
+      const f16x8_t n1a = bq[(TN + 1) % 3][0], n1b = bq[(TN + 1) % 3][1];
+      bq[0][0] = n0a;
+      bq[0][1] = n0b;
+      bq[1][0] = n1a;
+      bq[1][1] = n1b;
+    }
+    // this wave's W DMAs of tile kt + NSTAGE - 1 have landed (its A loads may still fly), then
+    // everyone's: that stage is readable, and this tile's stage is free for the next DMA
+    if constexpr ((ABL & 32) == 0) {
+      if (more_a && (ABL & (8 | 256)) == 0)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA_OPS) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr ((ABL & 128) == 0) __builtin_amdgcn_s_barrier();
+    }
+    st_cur = st_nx;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  float ainv[TM];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) ainv[mi] = 1.f / as[mi];
+  if (nsplit > 1) {  // split-K: this slice's partial sums, scaled back (the reduce adds the rest)
+    float* part = a.part + (size_t)kz * M * a.N;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int row = mi * 16 + 4 * g + v, col = ni * 16 + c16;
+          const float si = __shfl(ainv[mi], row & 15, 64);
+          const int m = m0 + wave * WM + row, n = n0 + col;
+          if (m < M) part[(size_t)m * a.N + n] = acc[mi][ni][v] * si * a.winv[n];
+        }
+    return;
+  }
+  __syncthreads();
+  h3_epilogue16<BM, BN, WM, BN, TM, TN, NT, EPI, false>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
+}
+
+template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int ABL = 0>
+inline int launch_conv_r3_cfg(const ConvArgs& a, hipStream_t st) {
+  if (!a.wh || !a.winv || a.Kpad % 32 != 0 || (a.nseg == 2 && a.kseg1 % 32 != 0) || a.N % BN != 0 || a.res_up) {
+    set_error("conv_r3: K/N not aligned to the tile, no split weights or an upsampled residual (Kpad=%d kseg1=%d N=%d)", a.Kpad,
+              a.kseg1, a.N);
+    return SFA_E_UNSUPPORTED;
+  }
+  for (int s = 0; s < a.nseg; ++s)
+    if (a.seg[s].C < 8) {  // a lane's 8 k values must be 8 channels of one input pixel
+      set_error("conv_r3: segment %d has C=%d < 8", s, a.seg[s].C);
+      return SFA_E_UNSUPPORTED;
+    }
+  if (a.wstride && (a.wstride < a.wk0 + a.Kpad || a.wk0 % 8 != 0)) {
+    set_error("conv_r3: K slice [%d, %d) outside the weight rows (stride %d)", a.wk0, a.wk0 + a.Kpad, a.wstride);
+    return SFA_E_INVALID;
+  }
+  if (2ull * a.N * (a.wstride ? a.wstride : a.Kpad) * 2ull >= (1ull << 31)) {
+    set_error("conv_r3: split weights >= 2 GiB");
+    return SFA_E_UNSUPPORTED;
+  }
+  const int ks = a.ksplit > 1 ? a.ksplit : 1;
+  if (ks > 1 && (EPI != EPI_STD || (a.Kpad / 32) % ks != 0 || !a.part ||
+                 (size_t)ks * a.M * a.N > a.part_floats || a.N % 4 != 0)) {
+    set_error("conv_r3: split-K %d unsupported here (Kpad=%d N=%d)", ks, a.Kpad, a.N);
+    return SFA_E_UNSUPPORTED;
+  }
+  const long long nblocks = (long long)ceil_div(a.M, BM) * (a.N / BN) * ks;
+  if (nblocks <= 0 || nblocks > 0x7fffffffll) {
+    set_error("conv_r3: bad grid (M=%d N=%d)", a.M, a.N);
+    return SFA_E_INVALID;
+  }
+  if (a.nseg == 2)
+    hipLaunchKernelGGL((conv_r3_kernel<BM, BN, WM, EPI, OCC, NSTAGE, 2, ABL>), dim3((unsigned)nblocks),
+                       dim3((BM / WM) * 64), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_r3_kernel<BM, BN, WM, EPI, OCC, NSTAGE, 1, ABL>), dim3((unsigned)nblocks),
+                       dim3((BM / WM) * 64), 0, st, a);
+  SFA_LAUNCH_CHECK();
+  if (ks > 1) {
+    const long long nel = (long long)a.M * a.N;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((nel + 1023) / 1024)), dim3(256), 0, st, a);
+    SFA_LAUNCH_CHECK();
+  }
+  return SFA_OK;
+}
+
+}  // namespace sfa

@@ -17,6 +17,7 @@
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_x6_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3s_kernel.h"
+#include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_r3_kernel.h"
 
 namespace sfa {
 void set_error(const char* fmt, ...) {
@@ -202,6 +203,17 @@ static const size_t g_part_floats = 64u << 20;
           return launch_conv_h3s_cfg<BM, BN, WM, EPI, OCC>(b, s);                                 \
         }                                                                                         \
   }
+#define CANDR(BM, BN, WM, EPI, OCC, NS, ABL, KS)                                                    \
+  Cand {                                                                                          \
+    "h3r " #BM "x" #BN " w" #WM " occ" #OCC " st" #NS " abl" #ABL " ks" #KS, 32,                    \
+        [](const ConvArgs& a, hipStream_t s) {                                                    \
+          ConvArgs b = a;                                                                         \
+          b.ksplit = KS;                                                                          \
+          b.part = g_part;                                                                        \
+          b.part_floats = g_part_floats;                                                          \
+          return launch_conv_r3_cfg<BM, BN, WM, EPI, OCC, NS, ABL>(b, s);                         \
+        }                                                                                         \
+  }
 #define CANDA(BM, BN, WM, WN, BK, EPI, OCC, ABL) CANDG(BM, BN, WM, WN, BK, EPI, OCC, false, ABL)
 #define CAND(BM, BN, WM, WN, BK, EPI, OCC) CANDA(BM, BN, WM, WN, BK, EPI, OCC, 0)
 
@@ -220,39 +232,28 @@ int main(int argc, char** argv) {
       {"head L2 3x3 64->5x64", 16, 152, 152, 64, 3, 1, 1, 320, true, false},
       {"head L0 3x3 256->5x64", 16, 76, 76, 256, 3, 1, 1, 320, true, false},
   };
+  // round 2: conv_r3_kernel (A in registers) against the round-1 defaults (first entry of each)
   std::vector<Cand> n64 = {
-      CAND(128, 64, 32, 64, 16, EPI_STD, 4),
-      CANDM(256, 64, 32, EPI_STD, 1, 2, 0), CANDM(256, 64, 32, EPI_STD, 1, 2, 1),
-      CANDN(256, 64, 32, EPI_STD, 1, 16, 3, false, 0), CANDN(256, 64, 32, EPI_STD, 1, 16, 3, false, 2),
-      CANDM(256, 64, 32, EPI_STD, 1, 3, 0), CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
-      CANDT(256, 64, 32, EPI_STD, 1, 1), CANDT(128, 64, 32, EPI_STD, 2, 1),
-      CANDT(128, 64, 32, EPI_STD, 3, 1), CANDT(64, 64, 32, EPI_STD, 4, 1), CANDT(64, 64, 16, EPI_STD, 4, 1),
-      CANDT(128, 64, 16, EPI_STD, 2, 1), CANDT(128, 64, 16, EPI_STD, 3, 1), CANDT(256, 64, 16, EPI_STD, 1, 1),
+      CANDT(128, 64, 32, EPI_STD, 3, 1),
+      CANDR(256, 64, 32, EPI_STD, 4, 2, 256, 1), CANDR(256, 64, 32, EPI_STD, 4, 3, 256, 1),
+      CANDR(128, 64, 32, EPI_STD, 4, 2, 256, 1), CANDR(128, 64, 32, EPI_STD, 2, 2, 256, 1),
+      CANDR(256, 64, 32, EPI_STD, 2, 2, 256, 1), CANDR(256, 64, 32, EPI_STD, 4, 2, 260, 1),
   };
   std::vector<Cand> stem = {
-      CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0), CANDN(128, 64, 32, EPI_STD, 3, 16, 3, false, 0),
-      CANDN(128, 64, 32, EPI_STD, 2, 16, 4, false, 0), CANDN(128, 64, 32, EPI_STD, 2, 32, 2, false, 0),
-      CANDM(128, 64, 32, EPI_STD, 2, 2, 2), CANDM(128, 64, 32, EPI_STD, 3, 2, 2), CANDM(128, 64, 32, EPI_STD, 2, 3, 2),
-      CANDM(256, 64, 32, EPI_STD, 1, 2, 2),
+      CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
   };
   std::vector<Cand> nbig = {
-      CAND(64, 128, 32, 64, 16, EPI_STD, 4),
-      CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2), CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 3),
-      CANDK(128, 128, 32, EPI_STD, 2, 2, 2, 0, 2), CANDK(128, 128, 32, EPI_STD, 2, 2, 2, 0, 4),
-      CANDK(128, 128, 32, EPI_STD, 2, 2, 2, 0, 8),
-      CANDT(128, 128, 32, EPI_STD, 2, 1), CANDT(256, 128, 32, EPI_STD, 1, 1),
-      CANDT(128, 128, 32, EPI_STD, 2, 2), CANDT(128, 128, 32, EPI_STD, 2, 4),
-      CANDT(64, 128, 32, EPI_STD, 4, 1), CANDT(64, 128, 16, EPI_STD, 3, 1),
-      CANDT(64, 128, 16, EPI_STD, 3, 2), CANDT(128, 128, 16, EPI_STD, 2, 1), CANDT(128, 128, 16, EPI_STD, 2, 2),
-      CANDT(64, 128, 16, EPI_STD, 2, 1),
-      CANDM(64, 128, 32, EPI_STD, 3, 2, 2), CANDM(128, 128, 32, EPI_STD, 2, 2, 2),
+      CANDT(128, 128, 32, EPI_STD, 2, 1), CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2),
+      CANDT(128, 128, 32, EPI_STD, 2, 2),
+      CANDR(128, 128, 32, EPI_STD, 2, 2, 256, 1), CANDR(128, 128, 32, EPI_STD, 2, 3, 256, 1),
+      CANDR(256, 128, 32, EPI_STD, 2, 2, 256, 1), CANDR(128, 128, 32, EPI_STD, 2, 2, 260, 1),
+      CANDR(128, 128, 32, EPI_STD, 2, 2, 256, 2), CANDR(64, 128, 16, EPI_STD, 4, 2, 256, 1),
   };
   std::vector<Cand> heads = {
-      CAND(128, 64, 32, 64, 16, EPI_HEAD, 4),
-      CANDM(256, 320, 32, EPI_HEAD, 1, 2, 2), CANDM(256, 320, 32, EPI_HEAD, 1, 2, 3),
-      CANDT(256, 320, 32, EPI_HEAD, 1, 1),
-      CANDW(256, 320, 64, 160, EPI_HEAD, 1, 2, 2), CANDW(256, 320, 32, 160, EPI_HEAD, 1, 2, 2),
-      CANDW(128, 320, 32, 160, EPI_HEAD, 1, 2, 2),
+      CANDM(256, 320, 32, EPI_HEAD, 1, 2, 2),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 256, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 768, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 772, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 260, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 256, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -326,6 +327,7 @@ int main(int argc, char** argv) {
     std::vector<Cand>& cands = sh.head ? heads : sh.C == 4 ? stem : (sh.N == 64 ? n64 : nbig);
     printf("\n== %s  M=%d N=%d K=%d  (%.2f GFLOP)\n", sh.name, M, sh.N, K, flop / 1e9);
     std::vector<float> ref, got;
+    ref.clear();
     for (size_t ci = 0; ci < cands.size(); ++ci) {
       Cand& c = cands[ci];
       a.Kpad = c.BK == 16 ? (K + 15) / 16 * 16 : Kpad;
@@ -358,7 +360,7 @@ int main(int argc, char** argv) {
       got.resize(ysz);
       CK(hipMemcpy(got.data(), y, ysz * 4, hipMemcpyDeviceToHost));
       double maxd = 0, maxr = 0;
-      if (ci == 0) {
+      if (ref.empty()) {  // the first supported candidate is the reference
         ref = got;
       } else {
         for (size_t i = 0; i < ysz; ++i) {
