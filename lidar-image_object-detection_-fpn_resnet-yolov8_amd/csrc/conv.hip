@@ -53,11 +53,11 @@ static bool strip_ok(const ConvArgs& a) {
 //  * the rest (stride-2 convs, 2-segment convs, 1x1 FPN convs, the stem): conv_h3_kernel,
 //    16x16x32 for the 64-wide ones, 32x32x16 for the 128..512-wide ones, BK 16 for the stem;
 //  * round 2: conv_r3_kernel (conv_r3_kernel.h: A fragments loaded straight into registers,
-//    only W through LDS, W DMA spread over the column blocks) for the heads (-7..8 % vs
-//    conv_h3_kernel), the 128-wide stride-1 layer2 convs (-10 % vs the strip kernel) and every
-//    128..512-wide conv the strip kernel cannot take (stride 2, conv + downsample segments,
-//    K-sliced FPN convs: -3..25 %; profiles/r02_convbench_*.txt); SFA_TUNE bits 4 / 16 / 8
-//    return those three groups to the round-1 kernels for same-box A/B;
+//    only W through LDS, W DMA spread over the column blocks, transposed accumulators) for the
+//    heads, the 128-wide stride-1 layer2 convs and the big-M (layer2) convs the strip kernel
+//    cannot take (stride 2, conv + downsample segments); on layer3/4 shapes it does not beat the
+//    strip / conv_h3 kernels (profiles/r02_convbench_*.txt). SFA_TUNE bits 4 / 16 / 8 return
+//    those three groups to the round-1 kernels for same-box A/B;
 //  * split-K 2 for the 512-wide (layer4) convs, whose 184 tiles cannot fill 256 CUs (-13..16 %);
 //    picked from the width only, so a frame's arithmetic never depends on the batch.
 // conv_x6g_kernel<..., PREC 1> tiles as the fallback.
@@ -70,6 +70,12 @@ static int tune_flags() {
   return f;
 }
 
+// conv_r3_kernel variants (conv_r3_kernel.h ABL bits): W DMA spread over the column blocks (256),
+// transposed accumulators with float4 / permlane-swap epilogues (2048); heads also s_setprio 1
+// for the second half of the waves (4).
+constexpr int R3_BODY = 256 | 2048;
+constexpr int R3_HEAD = 256 | 2048 | 4;
+
 static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;
   auto ok = [](int rc) { return rc != SFA_E_UNSUPPORTED; };
@@ -78,7 +84,7 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   const bool strip = strip_ok(a) && !sliced;
   if (epilogue == EPI_HEAD) {
     if (a.N == 320) {
-      if (!(tune_flags() & 4)) rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, 260>(a, st);
+      if (!(tune_flags() & 4)) rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD>(a, st);
       if (!ok(rc)) rc = launch_conv_h3_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2, 1>(a, st);
       if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 320, 32, EPI_HEAD, 1, 16, 3, 0, 320, 1>(a, st);
     }
@@ -100,12 +106,12 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     b.ksplit = a.part && a.N >= 512 && !sliced && a.bias ? 2 : 1;
     if (strip) {
       if (a.N == 128 && a.M >= 50000 && !(tune_flags() & 16))
-        rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, 256>(b, st);
+        rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
       else if (tune_flags() & 2)
         rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3>(b, st);
       if (!ok(rc)) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
-    } else if (!(tune_flags() & 8)) {  // stride-2 / two-segment / K-sliced: A from registers
-      rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, 256>(b, st);
+    } else if (a.M >= 50000 && !(tune_flags() & 8)) {  // big-M stride-2 / two-segment: A from registers
+      rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
     }
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
     if (!ok(rc) && b.ksplit > 1) {  // K not divisible into the slices: no split

@@ -20,7 +20,8 @@
 
 namespace sfa {
 
-template <int BM, int BN, int WM, int EPI, int OCC>
+// ABL (tools/convbench ablations only): 1 = no fp16x3 split (the f32 bits are fed to the MFMAs).
+template <int BM, int BN, int WM, int EPI, int OCC, int ABL = 0>
 __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const ConvArgs a) {
   constexpr int NW = BM / WM, NT = NW * 64;
   constexpr int TM = WM / 16, TN = BN / 16;
@@ -144,11 +145,16 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
         q0 = x6_f32x4{0.f, 0.f, 0.f, 0.f};
         q1 = q0;
       }
-      f16x4_t t0, t1, u0, u1;
-      split2h(q0, as[mi], t0, t1);
-      split2h(q1, as[mi], u0, u1);
-      hf[0][mi] = __builtin_shufflevector(t0, u0, 0, 1, 2, 3, 4, 5, 6, 7);
-      hf[1][mi] = __builtin_shufflevector(t1, u1, 0, 1, 2, 3, 4, 5, 6, 7);
+      if constexpr ((ABL & 1) != 0) {
+        hf[0][mi] = __builtin_bit_cast(f16x8_t, __builtin_shufflevector(q0, q0, 0, 1, 2, 3));
+        hf[1][mi] = __builtin_bit_cast(f16x8_t, __builtin_shufflevector(q1, q1, 0, 1, 2, 3));
+      } else {
+        f16x4_t t0, t1, u0, u1;
+        split2h(q0, as[mi], t0, t1);
+        split2h(q1, as[mi], u0, u1);
+        hf[0][mi] = __builtin_shufflevector(t0, u0, 0, 1, 2, 3, 4, 5, 6, 7);
+        hf[1][mi] = __builtin_shufflevector(t1, u1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
     }
     const unsigned char* SB = Sw + c16 * BROW + ((gq ^ swzB(c16)) << 4);
     f16x8_t bq[3][2];
@@ -217,7 +223,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
   h3_epilogue16<BM, BN, WM, BN, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
 }
 
-template <int BM, int BN, int WM, int EPI, int OCC>
+template <int BM, int BN, int WM, int EPI, int OCC, int ABL = 0>
 inline int launch_conv_h3s_cfg(const ConvArgs& a, hipStream_t st) {
   const ConvSeg& g = a.seg[0];
   const int ks = a.ksplit > 1 ? a.ksplit : 1;
@@ -241,8 +247,8 @@ inline int launch_conv_h3s_cfg(const ConvArgs& a, hipStream_t st) {
     set_error("conv_h3s: bad grid (M=%d N=%d)", a.M, a.N);
     return SFA_E_INVALID;
   }
-  hipLaunchKernelGGL((conv_h3s_kernel<BM, BN, WM, EPI, OCC>), dim3((unsigned)nblocks), dim3((BM / WM) * 64), 0, st,
-                     a);
+  hipLaunchKernelGGL((conv_h3s_kernel<BM, BN, WM, EPI, OCC, ABL>), dim3((unsigned)nblocks), dim3((BM / WM) * 64), 0,
+                     st, a);
   SFA_LAUNCH_CHECK();
   if (ks > 1) {
     const long long nel = (long long)a.M * a.N;

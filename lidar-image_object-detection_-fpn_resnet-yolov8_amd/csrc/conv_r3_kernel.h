@@ -32,12 +32,138 @@ namespace sfa {
 
 typedef unsigned r3_u32x4 __attribute__((ext_vector_type(4)));
 
+// Epilogues of the TRANSPOSED accumulator form (ABL 2048: the MFMAs take the W fragment as
+// their A operand and the activation fragment as B, so the 16x16 tile of acc[mi][ni] holds
+// C^T: lane l, register v -> output channel n0 + 16 ni + 4 (l >> 4) + v of pixel row
+// m0 + 16 mi + (l & 15)). Every lane owns four consecutive channels of ONE pixel: its own row
+// scale (no shuffle), float4 loads of bias / winv / residual and float4 stores of y (NHWC).
+template <int TM, int TN, int NT>
+__device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
+                                                 int mrow0, int m0, int n0, int lane, const float (&ainv)[TM]) {
+  const int M = a.M, c16 = lane & 15, g = lane >> 4;
+  AmaxRows am(a.OH * a.OW, m0);
+  x6_f32x4 rv[TM][TN];
+  if (a.res) {
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int m = min(mrow0 + mi * 16 + c16, M - 1);
+        rv[mi][ni] = *reinterpret_cast<const x6_f32x4*>(a.res + (size_t)m * a.N + n0 + ni * 16 + 4 * g);
+      }
+  }
+#pragma unroll
+  for (int ni = 0; ni < TN; ++ni) {
+    const int n = n0 + ni * 16 + 4 * g;
+    const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(a.winv + n);
+    const x6_f32x4 bn = a.bias ? *reinterpret_cast<const x6_f32x4*>(a.bias + n) : x6_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = mrow0 + mi * 16 + c16;
+      x6_f32x4 val;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float t = acc[mi][ni][v] * ainv[mi] * cs[v] + bn[v];
+        if (a.res) t += rv[mi][ni][v];
+        if (a.relu) t = fmaxf(t, 0.f);
+        val[v] = t;
+      }
+      if (m < M) {
+        *reinterpret_cast<x6_f32x4*>(a.y + (size_t)m * a.N + n) = val;
+        if (a.amax_out)
+          am.add(a.amax_out, m, fmaxf(fmaxf(fabsf(val[0]), fabsf(val[1])), fmaxf(fabsf(val[2]), fabsf(val[3]))));
+      }
+    }
+  }
+  if (a.amax_out) amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1, reinterpret_cast<float*>(smem));
+}
+
+// Heads (EPI_HEAD, transposed form): per head and pixel, ReLU(conv3x3 + b) of the lane's 16 of
+// the head's 64 channels and the 1x1 conv's partial sums over them (4 outputs x TM pixels),
+// reduced over the pixel's four lanes (l, l ^ 16, l ^ 32, l ^ 48) by v_permlane32/16_swap: each
+// swap exchanges half of a pair of partials, so two levels leave lane l >> 4 = o with output o
+// of both pixels (6 swaps + 6 adds, all VALU, no LDS, no barrier per head). The per-channel
+// weight scale winv = 2^-e (fp16x3) is folded into the staged 1x1 weights and biases
+// (w1 * winv, b / winv: exact power-of-two scalings), so T = max(acc * ainv + b', 0).
+template <int TM, int TN, int NT, int HPB>
+__device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
+                                                  int mrow0, int n0, int nt, int tid, const float (&ainv)[TM]) {
+  static_assert(TM == 2, "pairwise swap reduction assumes two 16-row sub-tiles per wave");
+  const int M = a.M, lane = tid & 63, c16 = lane & 15, g = lane >> 4;
+  float* WH = reinterpret_cast<float*>(smem);  // [HPB][4][64]: w1 * winv
+  float* BP = WH + HPB * 256;                  // [HPB * 64]: bias / winv
+  for (int i = tid; i < HPB * 256; i += NT) {
+    const int n = n0 + (i >> 8) * 64 + (i & 63);
+    WH[i] = a.hw1[nt * HPB * 256 + i] * a.winv[n];
+  }
+  for (int i = tid; i < HPB * 64; i += NT) BP[i] = a.bias[n0 + i] / a.winv[n0 + i];
+  __syncthreads();
+  auto swap_add32 = [](float& x, float& y) {  // x: sum over (l, l^32) in lanes < 32; y: in lanes >= 32
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  };
+  auto swap_add16 = [](float& x, float& y) {  // x: sum over (l, l^16) in even rows; y: odd rows
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(y), false, false);
+    x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  };
+#pragma unroll
+  for (int hh = 0; hh < HPB; ++hh) {
+    const int head = nt * HPB + hh;
+    int ch = 0, hoff = 0;
+#pragma unroll
+    for (int j = 0; j < SFA_MAX_HEADS; ++j)
+      if (j == head) {
+        ch = a.hch[j];
+        hoff = a.hoff[j];
+      }
+    float p[TM][4];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int o = 0; o < 4; ++o) p[mi][o] = 0.f;
+#pragma unroll
+    for (int ci = 0; ci < 4; ++ci) {
+      const int ni = 4 * hh + ci;
+      const int c = 16 * ci + 4 * g;  // channel within the head
+      const x6_f32x4 bp = *reinterpret_cast<const x6_f32x4*>(BP + hh * 64 + c);
+      x6_f32x4 w[4];
+#pragma unroll
+      for (int o = 0; o < 4; ++o) w[o] = *reinterpret_cast<const x6_f32x4*>(WH + hh * 256 + o * 64 + c);
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float t = fmaxf(fmaf(acc[mi][ni][v], ainv[mi], bp[v]), 0.f);
+#pragma unroll
+          for (int o = 0; o < 4; ++o) p[mi][o] = fmaf(t, w[o][v], p[mi][o]);
+        }
+    }
+    // level 1 (l ^ 32): lanes g < 2 keep outputs 0, 1, lanes g >= 2 outputs 2, 3
+    swap_add32(p[0][0], p[0][2]);
+    swap_add32(p[0][1], p[0][3]);
+    swap_add32(p[1][0], p[1][2]);
+    swap_add32(p[1][1], p[1][3]);
+    // level 2 (l ^ 16): even rows keep the first of each pair, odd rows the second -> lane g: output g
+    swap_add16(p[0][0], p[0][1]);
+    swap_add16(p[1][0], p[1][1]);
+    const float hb = a.hb1[head * 4 + g];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = mrow0 + mi * 16 + c16;
+      if (g < ch && m < M) a.hout[(size_t)(hoff + g) * M + m] = p[mi][0] + hb;
+    }
+  }
+}
+
 // ABL (tools/convbench variants): 1 = no W DMA in the K loop (ablation), 4 = s_setprio 1 for the
 // second half of the waves, 8 = do not pin the DMA / A-load placement (compiler scheduling; the
 // end-of-tile wait is then vmcnt(0), since the W DMAs are no longer known to precede the A loads),
 // 16 = split the next tile's A during this tile's MFMAs (hf / hn double buffer, +16 VGPRs),
 // 32 = pure MFMA stream (no loads, split, W reads or barriers in the K loop: the ceiling),
 // 64 = no split in the K loop (A loads kept live), 128 = no barrier in the K loop (ablations),
+// 1024 = no epilogue (accumulators kept live; ablation of the epilogue cost),
+// 2048 = transposed accumulators (W fragment as the MFMA A operand) with the float4 / shuffle
+// epilogues above,
 // 256 = spread the W DMA: A loads at block 0, then one W piece per block from block 2, the two
 // waves of a SIMD (w, w + NW/2) on alternate blocks, so no SIMD issues two DMA bursts at once,
 // 512 = staggered split: waves w < NW/2 split the next tile's A at block SPLIT_AT (into hn),
@@ -273,9 +399,15 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
         f32x4_t cc = acc[mi][ni];
-        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[1][mi], c0, cc, 0, 0, 0);
-        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c1, cc, 0, 0, 0);
-        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c0, cc, 0, 0, 0);
+        if constexpr ((ABL & 2048) != 0) {  // C^T: channels along the tile's rows
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[1][mi], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c1, hf[0][mi], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[0][mi], cc, 0, 0, 0);
+        } else {
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[1][mi], c0, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c1, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c0, cc, 0, 0, 0);
+        }
         acc[mi][ni] = cc;
       }
       if constexpr ((ABL & 16) != 0 && (ABL & 64) == 0) {
@@ -331,6 +463,21 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   float ainv[TM];
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi) ainv[mi] = 1.f / as[mi];
+  if (nsplit > 1 && (ABL & 2048) != 0) {  // split-K partials, transposed form: float4 per lane
+    float* part = a.part + (size_t)kz * M * a.N;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int m = m0 + wave * WM + mi * 16 + c16, n = n0 + ni * 16 + 4 * g;
+        const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(a.winv + n);
+        x6_f32x4 val;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) val[v] = acc[mi][ni][v] * ainv[mi] * cs[v];
+        if (m < M) *reinterpret_cast<x6_f32x4*>(part + (size_t)m * a.N + n) = val;
+      }
+    return;
+  }
   if (nsplit > 1) {  // split-K: this slice's partial sums, scaled back (the reduce adds the rest)
     float* part = a.part + (size_t)kz * M * a.N;
 #pragma unroll
@@ -346,8 +493,22 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
         }
     return;
   }
+  if constexpr ((ABL & 1024) != 0) {
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) asm volatile("" ::"v"(acc[mi][ni]));
+    return;
+  }
   __syncthreads();
-  h3_epilogue16<BM, BN, WM, BN, TM, TN, NT, EPI, false>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
+  if constexpr ((ABL & 2048) != 0) {
+    if constexpr (EPI == EPI_HEAD)
+      r3t_epilogue_head<TM, TN, NT, BN / 64>(a, acc, smem, m0 + wave * WM, n0, nt, tid, ainv);
+    else
+      r3t_epilogue_std<TM, TN, NT>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv);
+  } else {
+    h3_epilogue16<BM, BN, WM, BN, TM, TN, NT, EPI, false>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
+  }
 }
 
 template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int ABL = 0>

@@ -214,6 +214,11 @@ static const size_t g_part_floats = 64u << 20;
           return launch_conv_r3_cfg<BM, BN, WM, EPI, OCC, NS, ABL>(b, s);                         \
         }                                                                                         \
   }
+#define CANDTA(BM, BN, WM, EPI, OCC, ABL)                                                          \
+  Cand {                                                                                          \
+    "h3strip " #BM "x" #BN " w" #WM " occ" #OCC " abl" #ABL, 32,                                     \
+        [](const ConvArgs& a, hipStream_t s) { return launch_conv_h3s_cfg<BM, BN, WM, EPI, OCC, ABL>(a, s); } \
+  }
 #define CANDA(BM, BN, WM, WN, BK, EPI, OCC, ABL) CANDG(BM, BN, WM, WN, BK, EPI, OCC, false, ABL)
 #define CAND(BM, BN, WM, WN, BK, EPI, OCC) CANDA(BM, BN, WM, WN, BK, EPI, OCC, 0)
 
@@ -231,29 +236,24 @@ int main(int argc, char** argv) {
       {"head L1 3x3 128->5x64", 16, 152, 152, 128, 3, 1, 1, 320, true, false},
       {"head L2 3x3 64->5x64", 16, 152, 152, 64, 3, 1, 1, 320, true, false},
       {"head L0 3x3 256->5x64", 16, 76, 76, 256, 3, 1, 1, 320, true, false},
+      {"head tiny 3x3 8->5x64 (epilogue cost)", 16, 152, 152, 8, 3, 1, 1, 320, true, false},
   };
   // round 2: conv_r3_kernel (A in registers) against the round-1 defaults (first entry of each)
   std::vector<Cand> n64 = {
-      CANDT(128, 64, 32, EPI_STD, 3, 1),
-      CANDR(256, 64, 32, EPI_STD, 4, 2, 256, 1), CANDR(256, 64, 32, EPI_STD, 4, 3, 256, 1),
-      CANDR(128, 64, 32, EPI_STD, 4, 2, 256, 1), CANDR(128, 64, 32, EPI_STD, 2, 2, 256, 1),
-      CANDR(256, 64, 32, EPI_STD, 2, 2, 256, 1), CANDR(256, 64, 32, EPI_STD, 4, 2, 260, 1),
+      CANDT(128, 64, 32, EPI_STD, 3, 1), CANDTA(128, 64, 32, EPI_STD, 3, 1),
+      CANDT(128, 64, 32, EPI_STD, 2, 1), CANDTA(128, 64, 32, EPI_STD, 2, 1),
   };
   std::vector<Cand> stem = {
       CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
   };
   std::vector<Cand> nbig = {
-      CANDT(128, 128, 32, EPI_STD, 2, 1), CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2),
-      CANDT(128, 128, 32, EPI_STD, 2, 2),
-      CANDR(128, 128, 32, EPI_STD, 2, 2, 256, 1), CANDR(128, 128, 32, EPI_STD, 2, 3, 256, 1),
-      CANDR(256, 128, 32, EPI_STD, 2, 2, 256, 1), CANDR(128, 128, 32, EPI_STD, 2, 2, 260, 1),
-      CANDR(128, 128, 32, EPI_STD, 2, 2, 256, 2), CANDR(64, 128, 16, EPI_STD, 4, 2, 256, 1),
+      CANDR(128, 128, 32, EPI_STD, 2, 2, 256, 1), CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 1),
+      CANDR(128, 128, 32, EPI_STD, 2, 2, 256, 2), CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 2),
+      CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2),
   };
   std::vector<Cand> heads = {
-      CANDM(256, 320, 32, EPI_HEAD, 1, 2, 2),
-      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 256, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 768, 1),
-      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 772, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 260, 1),
-      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 256, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 260, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2308, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 3332, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
