@@ -54,10 +54,11 @@ static bool strip_ok(const ConvArgs& a) {
 //    16x16x32 for the 64-wide ones, 32x32x16 for the 128..512-wide ones, BK 16 for the stem;
 //  * round 2: conv_r3_kernel (conv_r3_kernel.h: A fragments loaded straight into registers,
 //    only W through LDS, W DMA spread over the column blocks, transposed accumulators) for the
-//    heads, the 128-wide stride-1 layer2 convs and the big-M (layer2) convs the strip kernel
-//    cannot take (stride 2, conv + downsample segments); on layer3/4 shapes it does not beat the
-//    strip / conv_h3 kernels (profiles/r02_convbench_*.txt). SFA_TUNE bits 4 / 16 / 8 return
-//    those three groups to the round-1 kernels for same-box A/B;
+//    heads and the big-M (layer2) convs the strip kernel cannot take (stride 2, conv +
+//    downsample segments); on layer3/4 shapes it does not beat the strip / conv_h3 kernels. The
+//    strip kernel runs in the transposed-accumulator form too (float4 epilogue: -7..11 %;
+//    profiles/r02_convbench_*.txt). SFA_TUNE bits 4 / 8 / 16 return the heads / the big-M
+//    non-strip convs / the strip convs to the round-1 kernels for same-box A/B;
 //  * split-K 2 for the 512-wide (layer4) convs, whose 184 tiles cannot fill 256 CUs (-13..16 %);
 //    picked from the width only, so a frame's arithmetic never depends on the batch.
 // conv_x6g_kernel<..., PREC 1> tiles as the fallback.
@@ -93,8 +94,9 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   }
   if (a.N == 64) {
     if (strip) {
-      if (tune_flags() & 1) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 2>(a, st);
-      else rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3>(a, st);
+      if (tune_flags() & 16) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3>(a, st);
+      else if (tune_flags() & 1) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 2, 2>(a, st);
+      else rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 2>(a, st);
     }
     if (!ok(rc) && a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 64, 32, EPI_STD, 2, 16, 3, false, 0>(a, st);
@@ -105,11 +107,11 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     ConvArgs b = a;
     b.ksplit = a.part && a.N >= 512 && !sliced && a.bias ? 2 : 1;
     if (strip) {
-      if (a.N == 128 && a.M >= 50000 && !(tune_flags() & 16))
-        rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
+      if (tune_flags() & 16)
+        rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
       else if (tune_flags() & 2)
-        rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3>(b, st);
-      if (!ok(rc)) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
+        rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3, 2>(b, st);
+      if (!ok(rc)) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, 2>(b, st);
     } else if (a.M >= 50000 && !(tune_flags() & 8)) {  // big-M stride-2 / two-segment: A from registers
       rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
     }

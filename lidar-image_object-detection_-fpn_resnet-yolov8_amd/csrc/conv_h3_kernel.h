@@ -240,8 +240,10 @@ __device__ __forceinline__ void h3_pool_epilogue(const ConvArgs& a, x6_f32x16 (&
 // WN (16x16x32 form only): columns per wave; WN < BN lays the waves out 2-D, (BM / WM) along M
 // times (BN / WN) along N, so each wave reads WN columns of W fragments instead of all BN
 // (fewer LDS bytes per MAC) and splits its WM rows of A.
+// RU: the epilogue handles an upsampled residual (a.res_up); instances without it (every conv but the
+// FPN skip convs) keep the residual tile in registers without spilling.
 template <int BM, int BN, int WM, int EPI, int OCC, int BK, int NSTAGE, int NSEG, bool NMAJ = false,
-          int ABL = 0, int MF = 0, int WN = BN>
+          int ABL = 0, int MF = 0, int WN = BN, bool RU = false>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_h3_kernel(const ConvArgs a) {
   static_assert(BK == 16 || BK == 32, "BK");
   static_assert(NSTAGE >= 2 && NSTAGE <= 4, "ring depth");
@@ -629,9 +631,9 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_h3_kerne
   if constexpr (EPI == EPI_POOL)
     h3_pool_epilogue<BM, BN, WM, TM, TN, NT>(a, acc, smem, m0, wave, tid, ainv);
   else if constexpr (MF == 1)
-    h3_epilogue16<BM, BN, WM, WN, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wm, wn, tid, ainv);
+    h3_epilogue16<BM, BN, WM, WN, TM, TN, NT, EPI, RU>(a, acc, smem, m0, n0, nt, wm, wn, tid, ainv);
   else
-    x6_epilogue<BM, BN, WM, BN, TM, TN, NT, EPI, 1>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
+    x6_epilogue<BM, BN, WM, BN, TM, TN, NT, EPI, 1, RU>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
 }
 
 // Split-K reduce: y = sum_z part[z] + bias (+ residual) (ReLU), per-frame max |y| — the
@@ -687,12 +689,20 @@ inline int launch_conv_h3_cfg(const ConvArgs& a, hipStream_t st) {
     set_error("conv_h3: bad grid (M=%d N=%d)", a.M, a.N);
     return SFA_E_INVALID;
   }
-  if (a.nseg == 2)
+  if (a.res_up) {  // FPN skip convs (one segment): the instance with the upsampled-residual epilogue
+    if (a.nseg != 1) {
+      set_error("conv_h3: upsampled residual with two K-segments");
+      return SFA_E_UNSUPPORTED;
+    }
+    hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 1, NMAJ, ABL, MF, WN, true>),
+                       dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WN) * 64), 0, st, a);
+  } else if (a.nseg == 2) {
     hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 2, NMAJ, ABL, MF, WN>),
                        dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WN) * 64), 0, st, a);
-  else
+  } else {
     hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 1, NMAJ, ABL, MF, WN>),
                        dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WN) * 64), 0, st, a);
+  }
   SFA_LAUNCH_CHECK();
   if (ks > 1) {
     const long long nel = (long long)a.M * a.N;

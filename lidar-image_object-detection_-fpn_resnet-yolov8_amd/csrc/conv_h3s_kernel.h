@@ -16,11 +16,13 @@
 // after W(t).  The last step re-issues its own tiles, so the counts stay uniform.
 #pragma once
 
-#include "conv_h3_kernel.h"
+#include "conv_r3_kernel.h"
 
 namespace sfa {
 
-// ABL (tools/convbench ablations only): 1 = no fp16x3 split (the f32 bits are fed to the MFMAs).
+// ABL: 1 = no fp16x3 split (the f32 bits are fed to the MFMAs; convbench ablation only),
+// 2 = transposed accumulators (W fragment as the MFMA A operand) with conv_r3_kernel.h's float4
+// epilogue (r3t_epilogue_std) and float4 split-K partials.
 template <int BM, int BN, int WM, int EPI, int OCC, int ABL = 0>
 __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const ConvArgs a) {
   constexpr int NW = BM / WM, NT = NW * 64;
@@ -37,6 +39,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
   constexpr int MAIN_BYTES = 2 * S_BYTES + 2 * W_BYTES;
   constexpr int LDS_BYTES = MAIN_BYTES > HEAD_BYTES ? MAIN_BYTES : HEAD_BYTES;
   static_assert(NW % 2 == 0 && WM % 16 == 0 && BN % 16 == 0, "tile");
+  static_assert((ABL & 2) == 0 || EPI == EPI_STD, "transposed form: standard epilogue only");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
 
   auto swzA = [](int R) { return ((R >> 1) & 7) ^ ((((R & 15) + 4) >> 2) & 2); };
@@ -171,9 +174,15 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
         f32x4_t cc = acc[mi][ni];
-        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[1][mi], c0, cc, 0, 0, 0);
-        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c1, cc, 0, 0, 0);
-        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c0, cc, 0, 0, 0);
+        if constexpr ((ABL & 2) != 0) {
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[1][mi], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c1, hf[0][mi], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[0][mi], cc, 0, 0, 0);
+        } else {
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[1][mi], c0, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c1, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c0, cc, 0, 0, 0);
+        }
         acc[mi][ni] = cc;
       }
       __builtin_amdgcn_sched_barrier(0);
@@ -204,6 +213,21 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (nsplit > 1 && (ABL & 2) != 0) {  // split-K partials, transposed form: float4 per lane
+    float* part = a.part + (size_t)kz * M * a.N;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int m = m0 + wave * WM + mi * 16 + c16, n = n0 + ni * 16 + 4 * gq;
+        const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(a.winv + n);
+        x6_f32x4 val;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) val[v] = acc[mi][ni][v] * ainv[mi] * cs[v];
+        if (m < M) *reinterpret_cast<x6_f32x4*>(part + (size_t)m * a.N + n) = val;
+      }
+    return;
+  }
   if (nsplit > 1) {  // split-K: this slice's partial sums, scaled back (the reduce adds the rest)
     float* part = a.part + (size_t)kz * M * a.N;
 #pragma unroll
@@ -220,7 +244,10 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     return;
   }
   __syncthreads();
-  h3_epilogue16<BM, BN, WM, BN, TM, TN, NT, EPI>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
+  if constexpr ((ABL & 2) != 0 && EPI == EPI_STD)
+    r3t_epilogue_std<TM, TN, NT>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv);
+  else
+    h3_epilogue16<BM, BN, WM, BN, TM, TN, NT, EPI, false>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
 }
 
 template <int BM, int BN, int WM, int EPI, int OCC, int ABL = 0>

@@ -65,7 +65,7 @@ __device__ __forceinline__ void split2h(const x6_f32x4 v, float s, f16x4_t& t0, 
 // PREC 1 (fp16x3): the accumulator of row R holds sum (x s_R)(w 2^e[n]); it is scaled
 // back by 1/s_R (ainv[mi] of the lane holding row R as its A row) and winv[n], both
 // powers of two, before the bias.  amax_out: the output's per-frame max |y| (conv.h).
-template <int BM, int BN, int WM, int WN, int TM, int TN, int NT, int EPI, int PREC = 0>
+template <int BM, int BN, int WM, int WN, int TM, int TN, int NT, int EPI, int PREC = 0, bool RES_UP = true>
 __device__ __forceinline__ void x6_epilogue(const ConvArgs& a, x6_f32x16 (&acc)[TM][TN],
                                             unsigned char* smem, int m0, int n0, int nt, int wm,
                                             int wn, int tid, const float (&ainv)[TM]) {
@@ -93,9 +93,11 @@ __device__ __forceinline__ void x6_epilogue(const ConvArgs& a, x6_f32x16 (&acc)[
             rv[mi][ni][v] = a.res[(size_t)m * a.N + n0 + wn * WN + ni * 32 + r];
           }
     }
-    if (a.res_up) {
 #pragma unroll
-      for (int ni = 0; ni < TN; ++ni)
+    for (int ni = 0; ni < TN; ++ni) {
+      // the upsampled residual (4 taps per value) is sampled per column block, not hoisted for the
+      // whole tile: that would hold 4 x TM x TN x 16 loads in registers and spill
+      if (RES_UP && a.res_up) {
 #pragma unroll
         for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
@@ -103,9 +105,7 @@ __device__ __forceinline__ void x6_epilogue(const ConvArgs& a, x6_f32x16 (&acc)[
             const int m = min(m0 + wm * WM + mi * 32 + (v & 3) + 8 * (v >> 2) + 4 * h, M - 1);
             rv[mi][ni][v] = res_up_sample(a, m, n0 + wn * WN + ni * 32 + r);
           }
-    }
-#pragma unroll
-    for (int ni = 0; ni < TN; ++ni) {
+      }
       const int n = n0 + wn * WN + ni * 32 + r;
       const float bn = a.bias ? a.bias[n] : 0.f;
       const float cs = PREC ? a.winv[n] : 1.f;
@@ -116,7 +116,7 @@ __device__ __forceinline__ void x6_epilogue(const ConvArgs& a, x6_f32x16 (&acc)[
           const int m = m0 + wm * WM + mi * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
           if (m < M) {
             float val = (PREC ? acc[mi][ni][v] * rinv[mi][v] * cs : acc[mi][ni][v]) + bn;
-            if (a.res || a.res_up) val += rv[mi][ni][v];
+            if (a.res || (RES_UP && a.res_up)) val += rv[mi][ni][v];
             if (a.relu) val = fmaxf(val, 0.f);
             a.y[(size_t)m * a.N + n] = val;
             if (a.amax_out) am.add(a.amax_out, m, val);

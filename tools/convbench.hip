@@ -219,6 +219,17 @@ static const size_t g_part_floats = 64u << 20;
     "h3strip " #BM "x" #BN " w" #WM " occ" #OCC " abl" #ABL, 32,                                     \
         [](const ConvArgs& a, hipStream_t s) { return launch_conv_h3s_cfg<BM, BN, WM, EPI, OCC, ABL>(a, s); } \
   }
+#define CANDTK(BM, BN, WM, EPI, OCC, ABL, KS)                                                      \
+  Cand {                                                                                          \
+    "h3strip " #BM "x" #BN " w" #WM " occ" #OCC " abl" #ABL " ks" #KS, 32,                          \
+        [](const ConvArgs& a, hipStream_t s) {                                                    \
+          ConvArgs b = a;                                                                         \
+          b.ksplit = KS;                                                                          \
+          b.part = g_part;                                                                        \
+          b.part_floats = g_part_floats;                                                          \
+          return launch_conv_h3s_cfg<BM, BN, WM, EPI, OCC, ABL>(b, s);                            \
+        }                                                                                         \
+  }
 #define CANDA(BM, BN, WM, WN, BK, EPI, OCC, ABL) CANDG(BM, BN, WM, WN, BK, EPI, OCC, false, ABL)
 #define CAND(BM, BN, WM, WN, BK, EPI, OCC) CANDA(BM, BN, WM, WN, BK, EPI, OCC, 0)
 
@@ -240,15 +251,16 @@ int main(int argc, char** argv) {
   };
   // round 2: conv_r3_kernel (A in registers) against the round-1 defaults (first entry of each)
   std::vector<Cand> n64 = {
-      CANDT(128, 64, 32, EPI_STD, 3, 1), CANDTA(128, 64, 32, EPI_STD, 3, 1),
-      CANDT(128, 64, 32, EPI_STD, 2, 1), CANDTA(128, 64, 32, EPI_STD, 2, 1),
+      CANDT(128, 64, 32, EPI_STD, 3, 1), CANDTA(128, 64, 32, EPI_STD, 3, 2),
+      CANDTA(128, 64, 32, EPI_STD, 2, 2), CANDTA(256, 64, 32, EPI_STD, 2, 2),
   };
   std::vector<Cand> stem = {
       CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
   };
   std::vector<Cand> nbig = {
-      CANDR(128, 128, 32, EPI_STD, 2, 2, 256, 1), CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 1),
-      CANDR(128, 128, 32, EPI_STD, 2, 2, 256, 2), CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 2),
+      CANDT(128, 128, 32, EPI_STD, 2, 1), CANDTA(128, 128, 32, EPI_STD, 2, 2),
+      CANDT(128, 128, 32, EPI_STD, 2, 2), CANDTK(128, 128, 32, EPI_STD, 2, 2, 2),
+      CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 1), CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 2),
       CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2),
   };
   std::vector<Cand> heads = {
