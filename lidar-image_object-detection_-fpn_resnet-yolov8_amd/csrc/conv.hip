@@ -95,8 +95,8 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (a.N == 64) {
     if (strip) {
       if (tune_flags() & 16) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3>(a, st);
-      else if (tune_flags() & 1) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 2, 2>(a, st);
-      else rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 2>(a, st);
+      else if (tune_flags() & 1) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 2>(a, st);
+      else rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 6>(a, st);  // + pre-split strip (-3 %)
     }
     if (!ok(rc) && a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 64, 32, EPI_STD, 2, 16, 3, false, 0>(a, st);

@@ -22,7 +22,11 @@ namespace sfa {
 
 // ABL: 1 = no fp16x3 split (the f32 bits are fed to the MFMAs; convbench ablation only),
 // 2 = transposed accumulators (W fragment as the MFMA A operand) with conv_r3_kernel.h's float4
-// epilogue (r3t_epilogue_std) and float4 split-K partials.
+// epilogue (r3t_epilogue_std) and float4 split-K partials,
+// 4 = pre-split strip: at kw 0 each wave splits ITS rows of the f32 strip (WM + 2 rows, the kw
+// halo included) once into fp16 hi / lo rows of a private LDS region, and the three kw k-steps
+// read ready fp16 fragments (a third of the split VALU; conv padding by reading a zero row).
+// One f32 strip buffer: the next strip is issued at kw 1, when every wave has split this one.
 template <int BM, int BN, int WM, int EPI, int OCC, int ABL = 0>
 __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const ConvArgs a) {
   constexpr int NW = BM / WM, NT = NW * 64;
@@ -36,7 +40,11 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
   constexpr int NS = (ND_S + NW - 1) / NW, NS_REM = ND_S % NW;
   constexpr int NB = (ND_B + NW - 1) / NW, NB_REM = ND_B % NW;
   constexpr int HEAD_BYTES = EPI == EPI_HEAD ? BM * 65 * 4 + (BN / 64) * 1024 : 0;  // h3_epilogue16
-  constexpr int MAIN_BYTES = 2 * S_BYTES + 2 * W_BYTES;
+  constexpr bool PS = (ABL & 4) != 0;
+  constexpr int PROWS = WM + 2;              // a wave's pre-split rows (its WM rows + the kw halo)
+  constexpr int PR_BYTES = (PROWS + 1) * 64;  // per term: 32 fp16 per row, + one zero row
+  constexpr int NSB = PS ? 1 : 2;             // f32 strip buffers
+  constexpr int MAIN_BYTES = NSB * S_BYTES + 2 * W_BYTES + (PS ? NW * 2 * PR_BYTES : 0);
   constexpr int LDS_BYTES = MAIN_BYTES > HEAD_BYTES ? MAIN_BYTES : HEAD_BYTES;
   static_assert(NW % 2 == 0 && WM % 16 == 0 && BN % 16 == 0, "tile");
   static_assert((ABL & 2) == 0 || EPI == EPI_STD, "transposed form: standard epilogue only");
@@ -98,6 +106,18 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     as[mi] = amax_frame_scale(a.amax_in, 1, m / (a.OH * a.OW), ainv[mi]);
   }
 
+  // pre-split (PS): scale of strip row j = the frame of output row m0 - 1 + j (a block spans at
+  // most two frames; rows of another frame than their consumer are always masked as padding)
+  const int P = a.OH * a.OW;
+  const int fb = (m0 / P + 1) * P;  // first row of the next frame
+  float sA = 1.f, sB = 1.f;
+  if constexpr (PS) {
+    float t;
+    sA = amax_frame_scale(a.amax_in, 1, m0 / P, t);
+    sB = fb < M ? amax_frame_scale(a.amax_in, 1, fb / P, t) : sA;
+  }
+  auto swzP = [](int R) { return ((R >> 2) & 1) << 1; };  // conflict-free at every kw row offset
+
   const int nchunk = g.C >> 5;
   const int nsl = 3 * nchunk / nsplit;  // this block's (kh, chunk) super-steps s0 .. s0 + nsl - 1
   const int s0 = kz * nsl;
@@ -136,10 +156,39 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
 #pragma unroll
       for (int v = 0; v < 4; ++v) acc[mi][ni][v] = 0.f;
 
+  unsigned char* const PH = smem + NSB * S_BYTES + 2 * W_BYTES + wave * 2 * PR_BYTES;  // PS: hi rows, lo + PR_BYTES
+  auto presplit = [&](const unsigned char* Ss) {
+    const int rr = lane >> 3, q = lane & 7;
+#pragma unroll
+    for (int p = 0; p < (PROWS + 7) / 8; ++p) {
+      const int r = 8 * p + rr;
+      if (r < PROWS) {
+        const int j = wave * WM + r;
+        const x6_f32x4 x = *reinterpret_cast<const x6_f32x4*>(Ss + j * AROW + ((q ^ swzA(j)) << 4));
+        f16x4_t hi, lo;
+        split2h(x, m0 - 1 + j >= fb ? sB : sA, hi, lo);
+        const int off = r * 64 + (((q >> 1) ^ swzP(r)) << 4) + (q & 1) * 8;
+        *reinterpret_cast<f16x4_t*>(PH + off) = hi;
+        *reinterpret_cast<f16x4_t*>(PH + PR_BYTES + off) = lo;
+      }
+    }
+  };
+  if constexpr (PS) {  // the zero rows (conv padding at kw 0 / 2)
+    if (lane < 8) *reinterpret_cast<x6_f32x4*>(PH + (lane & 4 ? PR_BYTES : 0) + PROWS * 64 + (lane & 3) * 16) =
+        x6_f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   auto compute = [&](const unsigned char* Ss, const unsigned char* Sw, int kw) {
     f16x8_t hf[2][TM];
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
+      if constexpr (PS) {
+        const bool pad = kw == 0 ? xm[mi] == 0 : (kw == 2 ? xm[mi] == W - 1 : false);
+        const int R = pad ? PROWS : mi * 16 + c16 + kw;
+        const int o = R * 64 + ((gq ^ swzP(R)) << 4);
+        hf[0][mi] = *reinterpret_cast<const f16x8_t*>(PH + o);
+        hf[1][mi] = *reinterpret_cast<const f16x8_t*>(PH + PR_BYTES + o);
+        continue;
+      }
       const int R = wave * WM + mi * 16 + c16 + kw;
       x6_f32x4 q0 = *reinterpret_cast<const x6_f32x4*>(Ss + R * AROW + (((2 * gq) ^ swzA(R)) << 4));
       x6_f32x4 q1 = *reinterpret_cast<const x6_f32x4*>(Ss + R * AROW + (((2 * gq + 1) ^ swzA(R)) << 4));
@@ -189,7 +238,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     }
   };
 
-  unsigned char* const WB = smem + 2 * S_BYTES;
+  unsigned char* const WB = smem + NSB * S_BYTES;
   load_strip(s0, smem);
   load_w(wk0(s0, 0), WB);
   for (int sl = 0; sl < nsl; ++sl) {
@@ -198,6 +247,23 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
 #pragma unroll
     for (int kw = 0; kw < 3; ++kw) {
       const int t = 3 * sl + kw;
+      if constexpr (PS) {
+        // kw 2: W(t) landed (the next strip, issued after it at kw 1, may still fly); else all
+        if (kw == 2) {
+          if (NS_REM == 0 || wave < NS_REM)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS - 1) : "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();
+        load_w(kw < 2 ? wk0(s, kw + 1) : (last ? wk0(s, 2) : wk0(s + 1, 0)), WB + ((t + 1) & 1) * W_BYTES);
+        if (kw == 1) load_strip(last ? s : s + 1, smem);  // every wave has split strip s
+        if (kw == 0) presplit(smem);
+        compute(smem, WB + (t & 1) * W_BYTES, kw);
+        continue;
+      }
       if (kw == 1) {
         if (NS_REM == 0 || wave < NS_REM)
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS) : "memory");
