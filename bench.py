@@ -444,7 +444,8 @@ def main():
             "roofline": {
                 "bound": "mfma",
                 "kernel": {"f32": "conv_mfma_kernel", "bf16x6": "conv_x6_kernel / conv_x6g_kernel",
-                           "fp16x3": "conv_h3_kernel"}.get(args.math, args.math) + " (math %s)" % args.math +
+                           "fp16x3": "conv_r3_kernel (heads, 49 % of the conv time) / conv_h3s_kernel / "
+                                     "conv_h3_kernel"}.get(args.math, args.math) + " (math %s)" % args.math +
                           (" (22 implicit-GEMM launches + the LDS-patch stem" if args.math == "fp16x3"
                            else " (23 implicit-GEMM launches") +
                           " per forward; achieved = algorithmic f32 FLOP "

@@ -264,8 +264,9 @@ int main(int argc, char** argv) {
       CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 1), CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2),
   };
   std::vector<Cand> heads = {
-      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 260, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2308, 1),
-      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 3332, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2308, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2340, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2309, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2372, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2436, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));

@@ -54,7 +54,7 @@ starts = [i for i, r in enumerate(merged) if "nchw3_to_nhwc4" in r["name"]]
 s = starts[-1]
 e = next(i for i in range(s, len(merged)) if "kfpn_combine" in merged[i]["name"])
 fwd = merged[s:e + 1]
-conv = [r for r in fwd if re.search(r"conv_(mfma|x6g?|h3s?)_kernel|splitk_reduce|stem_patch", r["name"])]
+conv = [r for r in fwd if re.search(r"conv_(mfma|x6g?|h3s?|r3)_kernel|splitk_reduce|stem_patch", r["name"])]
 
 
 def hbm(r):
