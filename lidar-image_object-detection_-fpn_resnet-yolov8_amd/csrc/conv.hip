@@ -75,7 +75,7 @@ static int tune_flags() {
 // transposed accumulators with float4 / permlane-swap epilogues (2048); heads also s_setprio 1
 // for the second half of the waves (4).
 constexpr int R3_BODY = 256 | 2048;
-constexpr int R3_HEAD = 256 | 2048 | 4;
+constexpr int R3_HEAD = 256 | 2048 | 4 | 4096;  // + the 2-VALU fp16 split (inline v_fma_mix)
 
 static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;
@@ -96,7 +96,7 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     if (strip) {
       if (tune_flags() & 16) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3>(a, st);
       else if (tune_flags() & 1) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 2>(a, st);
-      else rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 6>(a, st);  // + pre-split strip (-3 %)
+      else rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 14>(a, st);  // + pre-split strip, v_fma_mix split
     }
     if (!ok(rc) && a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 64, 32, EPI_STD, 2, 16, 3, false, 0>(a, st);
@@ -110,8 +110,8 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
       if (tune_flags() & 16)
         rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
       else if (tune_flags() & 2)
-        rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3, 2>(b, st);
-      if (!ok(rc)) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, 2>(b, st);
+        rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3, 10>(b, st);
+      if (!ok(rc)) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, 10>(b, st);  // transposed, v_fma_mix split
     } else if (a.M >= 50000 && !(tune_flags() & 8)) {  // big-M stride-2 / two-segment: A from registers
       rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
     }

@@ -27,6 +27,7 @@ namespace sfa {
 // halo included) once into fp16 hi / lo rows of a private LDS region, and the three kw k-steps
 // read ready fp16 fragments (a third of the split VALU; conv padding by reading a zero row).
 // One f32 strip buffer: the next strip is issued at kw 1, when every wave has split this one.
+// 8 = fp16 split in 2 VALU per value (split2h_x8 / split2h_pair, inline v_fma_mix).
 template <int BM, int BN, int WM, int EPI, int OCC, int ABL = 0>
 __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const ConvArgs a) {
   constexpr int NW = BM / WM, NT = NW * 64;
@@ -165,11 +166,21 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
       if (r < PROWS) {
         const int j = wave * WM + r;
         const x6_f32x4 x = *reinterpret_cast<const x6_f32x4*>(Ss + j * AROW + ((q ^ swzA(j)) << 4));
-        f16x4_t hi, lo;
-        split2h(x, m0 - 1 + j >= fb ? sB : sA, hi, lo);
+        const float sc = m0 - 1 + j >= fb ? sB : sA;
         const int off = r * 64 + (((q >> 1) ^ swzP(r)) << 4) + (q & 1) * 8;
-        *reinterpret_cast<f16x4_t*>(PH + off) = hi;
-        *reinterpret_cast<f16x4_t*>(PH + PR_BYTES + off) = lo;
+        if constexpr ((ABL & 8) != 0) {
+          typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+          unsigned h0, h1, l0, l1;
+          split2h_pair(x[0], x[1], sc, h0, l0);
+          split2h_pair(x[2], x[3], sc, h1, l1);
+          *reinterpret_cast<u32x2_t*>(PH + off) = u32x2_t{h0, h1};
+          *reinterpret_cast<u32x2_t*>(PH + PR_BYTES + off) = u32x2_t{l0, l1};
+        } else {
+          f16x4_t hi, lo;
+          split2h(x, sc, hi, lo);
+          *reinterpret_cast<f16x4_t*>(PH + off) = hi;
+          *reinterpret_cast<f16x4_t*>(PH + PR_BYTES + off) = lo;
+        }
       }
     }
   };
@@ -200,6 +211,8 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
       if constexpr ((ABL & 1) != 0) {
         hf[0][mi] = __builtin_bit_cast(f16x8_t, __builtin_shufflevector(q0, q0, 0, 1, 2, 3));
         hf[1][mi] = __builtin_bit_cast(f16x8_t, __builtin_shufflevector(q1, q1, 0, 1, 2, 3));
+      } else if constexpr ((ABL & 8) != 0) {
+        split2h_x8(q0, q1, as[mi], hf[0][mi], hf[1][mi]);
       } else {
         f16x4_t t0, t1, u0, u1;
         split2h(q0, as[mi], t0, t1);

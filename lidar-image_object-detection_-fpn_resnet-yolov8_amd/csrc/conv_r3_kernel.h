@@ -163,7 +163,7 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
 // 64 = no split in the K loop (A loads kept live), 128 = no barrier in the K loop (ablations),
 // 1024 = no epilogue (accumulators kept live; ablation of the epilogue cost),
 // 2048 = transposed accumulators (W fragment as the MFMA A operand) with the float4 / shuffle
-// epilogues above,
+// epilogues above, 4096 = fp16 split in 2 VALU per value (split2h_x8, inline v_fma_mix),
 // 256 = spread the W DMA: A loads at block 0, then one W piece per block from block 2, the two
 // waves of a SIMD (w, w + NW/2) on alternate blocks, so no SIMD issues two DMA bursts at once,
 // 512 = staggered split: waves w < NW/2 split the next tile's A at block SPLIT_AT (into hn),
@@ -303,11 +303,16 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   auto split_a = [&](f16x8_t (&h)[2][TM]) {
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
-      f16x4_t t0, t1, u0, u1;
-      split2h(__builtin_bit_cast(x6_f32x4, raw[mi][0]), as[mi], t0, t1);
-      split2h(__builtin_bit_cast(x6_f32x4, raw[mi][1]), as[mi], u0, u1);
-      h[0][mi] = __builtin_shufflevector(t0, u0, 0, 1, 2, 3, 4, 5, 6, 7);
-      h[1][mi] = __builtin_shufflevector(t1, u1, 0, 1, 2, 3, 4, 5, 6, 7);
+      if constexpr ((ABL & 4096) != 0) {  // 2 VALU per value (split2h_x8)
+        split2h_x8(__builtin_bit_cast(x6_f32x4, raw[mi][0]), __builtin_bit_cast(x6_f32x4, raw[mi][1]), as[mi],
+                   h[0][mi], h[1][mi]);
+      } else {
+        f16x4_t t0, t1, u0, u1;
+        split2h(__builtin_bit_cast(x6_f32x4, raw[mi][0]), as[mi], t0, t1);
+        split2h(__builtin_bit_cast(x6_f32x4, raw[mi][1]), as[mi], u0, u1);
+        h[0][mi] = __builtin_shufflevector(t0, u0, 0, 1, 2, 3, 4, 5, 6, 7);
+        h[1][mi] = __builtin_shufflevector(t1, u1, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
     }
   };
   // ABL 16: the next tile's A is split between the MFMAs of column block SPLIT_AT (into hn)

@@ -60,6 +60,30 @@ __device__ __forceinline__ void split2h(const x6_f32x4 v, float s, f16x4_t& t0, 
   }
 }
 
+// The same split in 2 VALU per value (hipcc mixes v_pk_mul / v_cvt_pk / v_cvt_f32_f16 / v_pk_fma
+// in and needs ~3.5): per pair, hi by v_fma_mixlo / mixhi (x s rounded once to fp16; x s is
+// exact), lo by the same with the fp16 hi as a negated third source (x s - hi is exact in f32,
+// rounded once). Bit-identical to split2h.
+__device__ __forceinline__ void split2h_pair(float x0, float x1, float s, unsigned& hi2, unsigned& lo2) {
+  asm("v_fma_mixlo_f16 %0, %2, %4, 0\n\t"
+      "v_fma_mixhi_f16 %0, %3, %4, 0\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(hi2), "=&v"(lo2)
+      : "v"(x0), "v"(x1), "v"(s));
+}
+// 8 f32 values (two quads) -> the fp16 hi / lo fragments (f16x8) of an MFMA operand
+__device__ __forceinline__ void split2h_x8(const x6_f32x4 q0, const x6_f32x4 q1, float s, f16x8_t& hi, f16x8_t& lo) {
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  unsigned h0, h1, h2, h3, l0, l1, l2, l3;
+  split2h_pair(q0[0], q0[1], s, h0, l0);
+  split2h_pair(q0[2], q0[3], s, h1, l1);
+  split2h_pair(q1[0], q1[1], s, h2, l2);
+  split2h_pair(q1[2], q1[3], s, h3, l3);
+  hi = __builtin_bit_cast(f16x8_t, u32x4_t{h0, h1, h2, h3});
+  lo = __builtin_bit_cast(f16x8_t, u32x4_t{l0, l1, l2, l3});
+}
+
 // Shared epilogue of the bf16x6 kernels (the accumulator layout of every 32x32 MFMA:
 // lane (r, h), register v -> row (v & 3) + 8 (v >> 2) + 4h, column r).
 // PREC 1 (fp16x3): the accumulator of row R holds sum (x s_R)(w 2^e[n]); it is scaled

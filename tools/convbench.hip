@@ -251,22 +251,18 @@ int main(int argc, char** argv) {
   };
   // round 2: conv_r3_kernel (A in registers) against the round-1 defaults (first entry of each)
   std::vector<Cand> n64 = {
-      CANDTA(128, 64, 32, EPI_STD, 3, 2), CANDTA(128, 64, 32, EPI_STD, 3, 6),
-      CANDTA(128, 64, 32, EPI_STD, 2, 6), CANDTA(256, 64, 32, EPI_STD, 2, 6),
-      CANDTA(128, 64, 64, EPI_STD, 4, 6),
+      CANDTA(128, 64, 32, EPI_STD, 3, 6), CANDTA(128, 64, 32, EPI_STD, 3, 14), CANDTA(128, 64, 32, EPI_STD, 3, 10),
   };
   std::vector<Cand> stem = {
       CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
   };
   std::vector<Cand> nbig = {
-      CANDTA(128, 128, 32, EPI_STD, 2, 2), CANDTA(128, 128, 32, EPI_STD, 2, 6),
-      CANDTK(128, 128, 32, EPI_STD, 2, 2, 2), CANDTK(128, 128, 32, EPI_STD, 2, 6, 2),
-      CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 1), CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2),
+      CANDTA(128, 128, 32, EPI_STD, 2, 2), CANDTA(128, 128, 32, EPI_STD, 2, 10),
+      CANDTK(128, 128, 32, EPI_STD, 2, 2, 2), CANDTK(128, 128, 32, EPI_STD, 2, 10, 2),
+      CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 1), CANDR(128, 128, 32, EPI_STD, 2, 2, 6400, 1),
   };
   std::vector<Cand> heads = {
-      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2308, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2340, 1),
-      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2309, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2372, 1),
-      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2436, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2308, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 6404, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
