@@ -75,7 +75,7 @@ static int tune_flags() {
 // transposed accumulators with float4 / permlane-swap epilogues (2048); heads also s_setprio 1
 // for the second half of the waves (4).
 constexpr int R3_BODY = 256 | 2048;
-constexpr int R3_HEAD = 256 | 2048 | 4 | 4096;  // + the 2-VALU fp16 split (inline v_fma_mix)
+constexpr int R3_HEAD = 256 | 2048 | 4 | 4096 | 8192 | 16384;  // + v_fma_mix split, 3-block W read-ahead, scalar tap decode
 
 static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;

@@ -27,7 +27,10 @@ namespace sfa {
 // halo included) once into fp16 hi / lo rows of a private LDS region, and the three kw k-steps
 // read ready fp16 fragments (a third of the split VALU; conv padding by reading a zero row).
 // One f32 strip buffer: the next strip is issued at kw 1, when every wave has split this one.
-// 8 = fp16 split in 2 VALU per value (split2h_x8 / split2h_pair, inline v_fma_mix).
+// 8 = fp16 split in 2 VALU per value (split2h_x8 / split2h_pair, inline v_fma_mix),
+// 16 = spread DMA: the k-step's W pieces (and the strip pieces, when due) are issued between the
+// MFMAs of column blocks 1, 2, .. (W first, then the strip: the counted waits are unchanged)
+// instead of in a burst right after the barrier.
 template <int BM, int BN, int WM, int EPI, int OCC, int ABL = 0>
 __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const ConvArgs a) {
   constexpr int NW = BM / WM, NT = NW * 64;
@@ -135,6 +138,22 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
       }
     }
   };
+  auto load_strip_piece = [&](int i, int s, unsigned char* S) {
+    const int kh = s / nchunk, c0 = (s - kh * nchunk) << 5;
+    if (NS_REM == 0 || i < NS - 1 || wave < NS_REM) {
+      const bool ok = (unsigned)(s_y[i] + kh - 1) < (unsigned)H;
+      const unsigned off =
+          ok ? (unsigned)((((s_pix[i] + (kh - 1) * W) << g.logC) + c0 + 4 * kq) << 2) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsx, (__attribute__((address_space(3))) void*)(S + (wave + NW * i) * 1024), 16, off, 0, 0, 0);
+    }
+  };
+  auto load_w_piece = [&](int jj, int k0, unsigned char* S) {
+    if (NB_REM == 0 || jj < NB - 1 || wave < NB_REM)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsw, (__attribute__((address_space(3))) void*)(S + (wave + NW * jj) * 1024), 16,
+          (unsigned)(boff[jj] + 2 * k0), 0, 0, 0);
+  };
   auto load_w = [&](int k0, unsigned char* S) {
 #pragma unroll
     for (int jj = 0; jj < NB; ++jj) {
@@ -188,7 +207,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     if (lane < 8) *reinterpret_cast<x6_f32x4*>(PH + (lane & 4 ? PR_BYTES : 0) + PROWS * 64 + (lane & 3) * 16) =
         x6_f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  auto compute = [&](const unsigned char* Ss, const unsigned char* Sw, int kw) {
+  auto compute = [&](const unsigned char* Ss, const unsigned char* Sw, int kw, auto&& issue) {
     f16x8_t hf[2][TM];
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
@@ -231,6 +250,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     if (TN > 1) read_b(1);
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
+      issue(ni);
       if (ni + 2 < TN) read_b(ni + 2);
       const f16x8_t c0 = bq[ni % 3][0], c1 = bq[ni % 3][1];
 #pragma unroll
@@ -251,6 +271,25 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     }
   };
 
+  // SPREAD: the pieces of a k-step, W first, then (when due) the strip, dealt over column blocks
+  // 1 .. TN - 1, PPB per block
+  constexpr bool SPREAD = (ABL & 16) != 0;
+  static_assert(!SPREAD || TN >= 2, "spread DMA needs two column blocks");
+  auto spread_issue = [&](int ni, bool with_strip, int wk, unsigned char* wdst, int snext, unsigned char* sdst) {
+    if (ni == 0) return;
+    constexpr int PPB_W = (NB + NS + TN - 2) / (TN - 1);  // pieces per block when the strip is due
+    constexpr int PPB_N = (NB + TN - 2) / (TN - 1);       // W only
+#pragma unroll
+    for (int u = 0; u < PPB_W; ++u) {
+      const int ppb = with_strip ? PPB_W : PPB_N;
+      if (u >= ppb) break;
+      const int pidx = (ni - 1) * ppb + u;
+      if (pidx < NB)
+        load_w_piece(pidx, wk, wdst);
+      else if (with_strip && pidx < NB + NS)
+        load_strip_piece(pidx - NB, snext, sdst);
+    }
+  };
   unsigned char* const WB = smem + NSB * S_BYTES;
   load_strip(s0, smem);
   load_w(wk0(s0, 0), WB);
@@ -271,10 +310,16 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         __builtin_amdgcn_s_barrier();
-        load_w(kw < 2 ? wk0(s, kw + 1) : (last ? wk0(s, 2) : wk0(s + 1, 0)), WB + ((t + 1) & 1) * W_BYTES);
-        if (kw == 1) load_strip(last ? s : s + 1, smem);  // every wave has split strip s
+        const int wnext = kw < 2 ? wk0(s, kw + 1) : (last ? wk0(s, 2) : wk0(s + 1, 0));
+        unsigned char* const wdst = WB + ((t + 1) & 1) * W_BYTES;
+        if constexpr (!SPREAD) {
+          load_w(wnext, wdst);
+          if (kw == 1) load_strip(last ? s : s + 1, smem);  // every wave has split strip s
+        }
         if (kw == 0) presplit(smem);
-        compute(smem, WB + (t & 1) * W_BYTES, kw);
+        compute(smem, WB + (t & 1) * W_BYTES, kw, [&](int ni) {
+          if constexpr (SPREAD) spread_issue(ni, kw == 1, wnext, wdst, last ? s : s + 1, smem);
+        });
         continue;
       }
       if (kw == 1) {
@@ -286,9 +331,16 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __builtin_amdgcn_s_barrier();  // W(t) (and the strip) landed for every wave; W(t-1) no longer read
-      load_w(kw < 2 ? wk0(s, kw + 1) : (last ? wk0(s, 2) : wk0(s + 1, 0)), WB + ((t + 1) & 1) * W_BYTES);
-      if (kw == 0) load_strip(last ? s : s + 1, smem + ((sl + 1) & 1) * S_BYTES);
-      compute(smem + (sl & 1) * S_BYTES, WB + (t & 1) * W_BYTES, kw);
+      const int wnext = kw < 2 ? wk0(s, kw + 1) : (last ? wk0(s, 2) : wk0(s + 1, 0));
+      unsigned char* const wdst = WB + ((t + 1) & 1) * W_BYTES;
+      unsigned char* const sdst = smem + ((sl + 1) & 1) * S_BYTES;
+      if constexpr (!SPREAD) {
+        load_w(wnext, wdst);
+        if (kw == 0) load_strip(last ? s : s + 1, sdst);
+      }
+      compute(smem + (sl & 1) * S_BYTES, WB + (t & 1) * W_BYTES, kw, [&](int ni) {
+        if constexpr (SPREAD) spread_issue(ni, kw == 0, wnext, wdst, last ? s : s + 1, sdst);
+      });
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -162,6 +162,9 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
 // 32 = pure MFMA stream (no loads, split, W reads or barriers in the K loop: the ceiling),
 // 64 = no split in the K loop (A loads kept live), 128 = no barrier in the K loop (ablations),
 // 1024 = no epilogue (accumulators kept live; ablation of the epilogue cost),
+// 16384 = scalar tap decode + per-lane tap validity masks for the A addresses (one segment,
+// C >= 32, checked at launch),
+// 8192 = W fragments read 3 column blocks ahead (4-slot ring, NSTAGE 2) instead of 2,
 // 2048 = transposed accumulators (W fragment as the MFMA A operand) with the float4 / shuffle
 // epilogues above, 4096 = fp16 split in 2 VALU per value (split2h_x8, inline v_fma_mix),
 // 256 = spread the W DMA: A loads at block 0, then one W piece per block from block 2, the two
@@ -252,6 +255,39 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   }
 
   r3_u32x4 raw[TM][2];  // A fragment of the next K-tile (f32 bits)
+  // ABL 16384 (one segment, C >= 32: a K-tile lies in one tap): the tap decode is wave-uniform
+  // (scalar), and each lane keeps a validity bit per tap and sub-tile row and the byte offset of
+  // its pixel + channel group, so an A address costs a bit test, an add and a select.
+  constexpr bool FAST_A = (ABL & 16384) != 0 && NSEG == 1;  // two-segment launches are refused
+  unsigned vmask[TM], abase[TM];
+  if constexpr (FAST_A) {
+    const ConvSeg& sg0 = a.seg[0];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int ih = r_ihw[0][mi] >> 16;
+      const int iw = (int)(short)(r_ihw[0][mi] & 0xffff);
+      unsigned msk = 0;
+      for (int t = 0; t < sg0.taps && t < 32; ++t) {
+        const int kh = (t * sg0.kdiv_mul) >> sg0.kdiv_sh, kw = t - kh * sg0.KW;
+        if ((unsigned)(ih + kh) < (unsigned)sg0.H && (unsigned)(iw + kw) < (unsigned)sg0.W) msk |= 1u << t;
+      }
+      vmask[mi] = msk;
+      abase[mi] = (unsigned)(((r_pix[0][mi] << sg0.logC) + 8 * g) << 2);
+    }
+  }
+  auto load_a_fast = [&](int k0) {
+    const ConvSeg& sg0 = a.seg[0];
+    const int tap = k0 >> sg0.logC, c0 = k0 & (sg0.C - 1);
+    const int kh = (tap * sg0.kdiv_mul) >> sg0.kdiv_sh, kw = tap - kh * sg0.KW;
+    const unsigned toff = (unsigned)((((kh * sg0.W + kw) << sg0.logC) + c0) << 2);
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const bool ok = tap < 32 && ((vmask[mi] >> tap) & 1u);
+      const unsigned off = ok ? abase[mi] + toff : 0x80000000u;
+      raw[mi][0] = __builtin_amdgcn_raw_buffer_load_b128(rs0, off, 0, 0);
+      raw[mi][1] = __builtin_amdgcn_raw_buffer_load_b128(rs0, off + 16u, 0, 0);
+    }
+  };
   auto load_a_seg = [&](auto sgc, const __amdgpu_buffer_rsrc_t rs, int kl) {
     constexpr int SG = decltype(sgc)::value;
     const ConvSeg& sgm = a.seg[SG];
@@ -274,7 +310,9 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   };
   auto load_a = [&](int kt) {
     const int k0 = kt * BK;
-    if constexpr (NSEG == 2) {
+    if constexpr (FAST_A) {
+      load_a_fast(k0);
+    } else if constexpr (NSEG == 2) {
       if (k0 >= a.kseg1)
         load_a_seg(std::integral_constant<int, 1>(), rs1, k0 - a.kseg1);
       else
@@ -328,7 +366,10 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
       for (int v = 0; v < 4; ++v) acc[mi][ni][v] = 0.f;
 
   const int bfo = c16 * BROW + ((g ^ swzB(c16)) << 4);  // this lane's W fragment in a block
-  f16x8_t bq[3][2];  // W fragment ring: block p in slot p % 3
+  constexpr int RA = (ABL & 8192) != 0 ? 3 : 2;  // W fragment blocks read ahead of their MFMAs
+  constexpr int RS = RA + 1;
+  static_assert(RA == 2 || NSTAGE == 2, "3-block read-ahead: NSTAGE 2 only");
+  f16x8_t bq[RS][2];  // W fragment ring: block p in slot p % RS
   auto read_b = [&](const unsigned char* S, int ni, f16x8_t (&dst)[2]) {
     dst[0] = *reinterpret_cast<const f16x8_t*>(S + bfo + ni * 16 * BROW);
     dst[1] = *reinterpret_cast<const f16x8_t*>(S + TERM_B + bfo + ni * 16 * BROW);
@@ -371,8 +412,8 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
     // for DMAs issued just before it (it counts the conditional DMA path conservatively)
     if constexpr ((ABL & 8) == 0) __builtin_amdgcn_sched_barrier(0);
     if constexpr (NSTAGE == 2) {
-      read_b(S, 0, bq[0]);
-      read_b(S, 1, bq[1]);
+#pragma unroll
+      for (int p = 0; p < RA; ++p) read_b(S, p, bq[p]);
     }
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
@@ -393,14 +434,14 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
           }
         }
       }
-      const int p = ni + 2;
+      const int p = ni + RA;
       if ((ABL & 32) != 0) {
-        asm volatile("" : "+v"(bq[p % 3][0]), "+v"(bq[p % 3][1]));
+        asm volatile("" : "+v"(bq[p % RS][0]), "+v"(bq[p % RS][1]));
       } else if (p < TN)
-        read_b(S, p, bq[p % 3]);
+        read_b(S, p, bq[p % RS]);
       else if (NSTAGE == 3 && more_a)
-        read_b(smem + st_nx * STAGE, p - TN, bq[p % 3]);
-      const f16x8_t c0 = bq[ni % 3][0], c1 = bq[ni % 3][1];
+        read_b(smem + st_nx * STAGE, p - TN, bq[p % RS]);
+      const f16x8_t c0 = bq[ni % RS][0], c1 = bq[ni % RS][1];
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
         f32x4_t cc = acc[mi][ni];
@@ -521,6 +562,10 @@ inline int launch_conv_r3_cfg(const ConvArgs& a, hipStream_t st) {
   if (!a.wh || !a.winv || a.Kpad % 32 != 0 || (a.nseg == 2 && a.kseg1 % 32 != 0) || a.N % BN != 0 || a.res_up) {
     set_error("conv_r3: K/N not aligned to the tile, no split weights or an upsampled residual (Kpad=%d kseg1=%d N=%d)", a.Kpad,
               a.kseg1, a.N);
+    return SFA_E_UNSUPPORTED;
+  }
+  if ((ABL & 16384) != 0 && (a.nseg != 1 || a.seg[0].C < 32 || a.seg[0].taps > 32)) {
+    set_error("conv_r3: fast A addressing needs one segment with C >= 32 (C=%d)", a.seg[0].C);
     return SFA_E_UNSUPPORTED;
   }
   for (int s = 0; s < a.nseg; ++s)

@@ -251,18 +251,17 @@ int main(int argc, char** argv) {
   };
   // round 2: conv_r3_kernel (A in registers) against the round-1 defaults (first entry of each)
   std::vector<Cand> n64 = {
-      CANDTA(128, 64, 32, EPI_STD, 3, 6), CANDTA(128, 64, 32, EPI_STD, 3, 14), CANDTA(128, 64, 32, EPI_STD, 3, 10),
+      CANDTA(128, 64, 32, EPI_STD, 3, 14), CANDTA(128, 64, 32, EPI_STD, 3, 30),
   };
   std::vector<Cand> stem = {
       CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
   };
   std::vector<Cand> nbig = {
-      CANDTA(128, 128, 32, EPI_STD, 2, 2), CANDTA(128, 128, 32, EPI_STD, 2, 10),
-      CANDTK(128, 128, 32, EPI_STD, 2, 2, 2), CANDTK(128, 128, 32, EPI_STD, 2, 10, 2),
-      CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 1), CANDR(128, 128, 32, EPI_STD, 2, 2, 6400, 1),
+      CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 1), CANDR(128, 128, 32, EPI_STD, 2, 2, 18688, 1),
+      CANDR(128, 128, 32, EPI_STD, 2, 2, 10496, 1),
   };
   std::vector<Cand> heads = {
-      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 2308, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 6404, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 14596, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 30980, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
