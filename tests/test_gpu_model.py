@@ -256,3 +256,31 @@ def test_fpn_commute_matches_concat_conv(golden, gpu, monkeypatch):
         scale = np.maximum(1.0, np.abs(r))
         assert float(np.max(np.abs(outs[0][h] - outs[1][h]) / scale)) <= 2e-5, h
         assert float(np.max(np.abs(outs[0][h] - r) / scale)) <= 1e-4, h
+
+
+@pytest.mark.parametrize("hw", [(160, 192), (96, 96)])
+def test_round2_kernels_match_round1(golden, gpu, monkeypatch, hw):
+    """Round-2 conv kernels (conv_r3_kernel for the heads and the big-M non-strip convs, the
+    transposed / pre-split strip kernel) == the round-1 kernels (SFA_TUNE=28: conv_h3_kernel,
+    the plain strip kernel) to f32 rounding (the head epilogue sums the 1x1 conv in another
+    order), both within the 1e-4 bar of the CPU reference. Odd sizes: partial last row tiles,
+    tiles spanning two frames, every image border of the register-A loads."""
+    from oracle import model_oracle
+    x = torch.from_numpy(synthetic.synthetic_bev(3, hw[0], hw[1], seed=29)).to(gpu)
+    outs = []
+    for flag in ("0", "28"):
+        monkeypatch.setenv("SFA_TUNE", flag)
+        model = make_model(golden, gpu)
+        model._engine(gpu).set_math(_math("fp16x3"))
+        with torch.no_grad():
+            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
+    sd = gc.state_dict_np(golden.model)
+    ref = model_oracle.forward(model_oracle.state_dict_torch(sd), x.cpu(), dict(gc.HEADS))
+    for h in gc.HEADS:
+        r = ref[h].numpy()
+        scale = np.maximum(1.0, np.abs(r))
+        d = float(np.max(np.abs(outs[0][h] - outs[1][h]) / scale))
+        e = float(np.max(np.abs(outs[0][h] - r) / scale))
+        print(f"round-2 vs round-1 kernels {hw} {h}: {d:.3g}, vs reference {e:.3g}")
+        assert d <= 2e-5, h
+        assert e <= 1e-4, h

@@ -257,8 +257,10 @@ int main(int argc, char** argv) {
       CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
   };
   std::vector<Cand> nbig = {
-      CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 1), CANDR(128, 128, 32, EPI_STD, 2, 2, 18688, 1),
-      CANDR(128, 128, 32, EPI_STD, 2, 2, 10496, 1),
+      CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 1),
+      CANDR(128, 128, 32, EPI_STD, 3, 2, 2304, 1), CANDR(128, 64, 32, EPI_STD, 3, 2, 2304, 1),
+      CANDTA(128, 64, 32, EPI_STD, 3, 10), CANDTK(128, 128, 32, EPI_STD, 2, 10, 2),
+      CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2),
   };
   std::vector<Cand> heads = {
       CANDR(256, 320, 32, EPI_HEAD, 1, 2, 14596, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 30980, 1),
