@@ -189,7 +189,7 @@ __device__ __forceinline__ float res_up_sample(const ConvArgs& a, int m, int n) 
   const float* r = a.res_up + (size_t)b * H * W * a.N + n;
   const float a00 = r[(y0 * W + x0) * a.N], a01 = r[(y0 * W + x1) * a.N];
   const float a10 = r[(y1 * W + x0) * a.N], a11 = r[(y1 * W + x1) * a.N];
-  return ly0 * (lx0 * a00 + lx1 * a01) + ly1 * (lx0 * a10 + lx1 * a11);
+  return fmaf(ly0, fmaf(lx0, a00, lx1 * a01), ly1 * fmaf(lx0, a10, lx1 * a11));  // as r3t_epilogue_std
 }
 
 int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t stream);

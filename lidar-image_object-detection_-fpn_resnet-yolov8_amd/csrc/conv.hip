@@ -11,6 +11,12 @@
 
 namespace sfa {
 
+// Tile choices are priced at the bench batch (16 frames of the launch's geometry), never at
+// a.M: different kernels sum in different orders, so a choice by the batch's row count would
+// let a frame's result depend on the batch it is computed in (tests/test_gpu_model.py
+// test_batch_invariance_608 holds every path to bit-identical frames across batches).
+static long long tile_rows(const ConvArgs& a) { return 16LL * a.OH * a.OW; }
+
 // bf16x6 tiles per shape, from tools/convbench.hip sweeps on MI355X (round 1):
 // wide-N tiles amortise the A split; 8-wave LDS-DMA tiles for the big-M layers.
 // Returns SFA_E_UNSUPPORTED when no bf16x6 tile fits (the caller falls back to f32).
@@ -26,8 +32,8 @@ static int launch_conv_x6(const ConvArgs& a, int epilogue, hipStream_t st) {
   }
   if (a.N == 64) return launch_conv_x6g_cfg<256, 64, 32, EPI_STD, 1>(a, st);
   if (a.N % 128 == 0) {
-    if (a.M >= 50000) rc = launch_conv_x6_cfg<128, 128, 64, 64, 16, EPI_STD, 2>(a, st);
-    else if (a.M >= 10000) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2>(a, st);
+    if (tile_rows(a) >= 50000) rc = launch_conv_x6_cfg<128, 128, 64, 64, 16, EPI_STD, 2>(a, st);
+    else if (tile_rows(a) >= 10000) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2>(a, st);
     else rc = launch_conv_x6_cfg<64, 128, 32, 64, 32, EPI_STD, 2>(a, st);
     if (!ok(rc)) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2>(a, st);
   }
@@ -74,6 +80,7 @@ static int tune_flags() {
 // transposed accumulators with float4 / permlane-swap epilogues (2048); heads also s_setprio 1
 // for the second half of the waves (4).
 constexpr int R3_BODY = 256 | 2048;
+constexpr int R3_FPN = 256 | 2048 | 32768;  // + the upsampled-residual epilogue (FPN skip convs)
 constexpr int R3_HEAD = 256 | 2048 | 4 | 4096 | 8192 | 16384;  // + v_fma_mix split, 3-block W read-ahead, scalar tap decode
 
 static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
@@ -90,6 +97,13 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     }
     if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_HEAD, 1, 16, 3, 0, 64, 1>(a, st);
     return rc;
+  }
+  if (a.res_up && !(tune_flags() & 32)) {  // FPN skip convs: transposed float4 epilogue, float4 taps
+    if (a.N == 64)
+      rc = launch_conv_r3_cfg<128, 64, 32, EPI_STD, 4, 2, R3_FPN>(a, st);
+    else if (a.N % 128 == 0)
+      rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_FPN>(a, st);
+    if (ok(rc)) return rc;
   }
   if (a.N == 64) {
     if (strip) {
@@ -111,7 +125,7 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
       else if (tune_flags() & 2)
         rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3, 10>(b, st);
       if (!ok(rc)) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, 10>(b, st);  // transposed, v_fma_mix split
-    } else if (a.M >= 50000 && !(tune_flags() & 8)) {  // big-M stride-2 / two-segment: A from registers
+    } else if (tile_rows(a) >= 50000 && !(tune_flags() & 8)) {  // big-M stride-2 / two-segment: A from registers
       rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
     }
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
@@ -190,9 +204,9 @@ int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t st) {
   }
   if (a.N == 64) return launch_conv_cfg<128, 64, 32, 64, 16, EPI_STD, 4>(a, st);
   if (a.N % 128 == 0) {
-    if ((long long)ceil_div(a.M, 128) * (a.N / 128) >= 512)
+    if ((tile_rows(a) + 127) / 128 * (a.N / 128) >= 512)
       return launch_conv_cfg<128, 128, 64, 64, 16, EPI_STD, 3>(a, st);
-    if ((long long)ceil_div(a.M, 64) * (a.N / 128) >= 512)
+    if ((tile_rows(a) + 63) / 64 * (a.N / 128) >= 512)
       return launch_conv_cfg<64, 128, 32, 64, 16, EPI_STD, 4, true>(a, st);
     if (a.Kpad % 32 == 0 && (a.nseg == 1 || a.kseg1 % 32 == 0))
       return launch_conv_cfg<64, 64, 32, 32, 32, EPI_STD, 4>(a, st);

@@ -37,12 +37,46 @@ typedef unsigned r3_u32x4 __attribute__((ext_vector_type(4)));
 // C^T: lane l, register v -> output channel n0 + 16 ni + 4 (l >> 4) + v of pixel row
 // m0 + 16 mi + (l & 15)). Every lane owns four consecutive channels of ONE pixel: its own row
 // scale (no shuffle), float4 loads of bias / winv / residual and float4 stores of y (NHWC).
-template <int TM, int TN, int NT>
+// RU: the residual may also be given at half resolution (a.res_up, the FPN skip convs), added
+// bilinearly upsampled x2 (align_corners) exactly as res_up_sample evaluates it, 4 float4 taps
+// per lane and column block (the 4 channels of the lane).
+template <int TM, int TN, int NT, bool RU = false>
 __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
                                                  int mrow0, int m0, int n0, int lane, const float (&ainv)[TM]) {
+  // every element is evaluated by the same rounding sequence (explicit fmaf, no contraction):
+  // left to the compiler, the unrolled copies were contracted differently (some mul + add, some
+  // fma, some packed), so a pixel's value depended on its row within the tile, i.e. on the
+  // batch it was computed in
+#pragma clang fp contract(off)
   const int M = a.M, c16 = lane & 15, g = lane >> 4;
   AmaxRows am(a.OH * a.OW, m0);
   x6_f32x4 rv[TM][TN];
+  if (RU && a.res_up) {
+    const int H = a.OH >> 1, W = a.OW >> 1;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = min(mrow0 + mi * 16 + c16, M - 1);
+      const int ow = m % a.OW, t = m / a.OW;
+      const int oh = t % a.OH, b = t / a.OH;
+      const float fy = a.res_sh * (float)oh, fx = a.res_sw * (float)ow;
+      const int y0 = (int)fy, x0 = (int)fx;
+      const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+      const float ly1 = fy - (float)y0, lx1 = fx - (float)x0;
+      const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+      const float* r = a.res_up + (size_t)b * H * W * a.N;
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int n = n0 + ni * 16 + 4 * g;
+        const x6_f32x4 a00 = *reinterpret_cast<const x6_f32x4*>(r + (size_t)(y0 * W + x0) * a.N + n);
+        const x6_f32x4 a01 = *reinterpret_cast<const x6_f32x4*>(r + (size_t)(y0 * W + x1) * a.N + n);
+        const x6_f32x4 a10 = *reinterpret_cast<const x6_f32x4*>(r + (size_t)(y1 * W + x0) * a.N + n);
+        const x6_f32x4 a11 = *reinterpret_cast<const x6_f32x4*>(r + (size_t)(y1 * W + x1) * a.N + n);
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          rv[mi][ni][v] = fmaf(ly0, fmaf(lx0, a00[v], lx1 * a01[v]), ly1 * fmaf(lx0, a10[v], lx1 * a11[v]));
+      }
+    }
+  }
   if (a.res) {
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
@@ -63,8 +97,8 @@ __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&ac
       x6_f32x4 val;
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        float t = acc[mi][ni][v] * ainv[mi] * cs[v] + bn[v];
-        if (a.res) t += rv[mi][ni][v];
+        float t = fmaf(acc[mi][ni][v] * ainv[mi], cs[v], bn[v]);  // acc * ainv: exact (power of two)
+        if (a.res || (RU && a.res_up)) t += rv[mi][ni][v];
         if (a.relu) t = fmaxf(t, 0.f);
         val[v] = t;
       }
@@ -162,6 +196,8 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
 // 32 = pure MFMA stream (no loads, split, W reads or barriers in the K loop: the ceiling),
 // 64 = no split in the K loop (A loads kept live), 128 = no barrier in the K loop (ablations),
 // 1024 = no epilogue (accumulators kept live; ablation of the epilogue cost),
+// 32768 = (with 2048) the epilogue also takes an upsampled half-resolution residual (a.res_up:
+// the FPN skip convs; only those instances carry its registers),
 // 16384 = scalar tap decode + per-lane tap validity masks for the A addresses (one segment,
 // C >= 32, checked at launch),
 // 8192 = W fragments read 3 column blocks ahead (4-slot ring, NSTAGE 2) instead of 2,
@@ -551,7 +587,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
     if constexpr (EPI == EPI_HEAD)
       r3t_epilogue_head<TM, TN, NT, BN / 64>(a, acc, smem, m0 + wave * WM, n0, nt, tid, ainv);
     else
-      r3t_epilogue_std<TM, TN, NT>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv);
+      r3t_epilogue_std<TM, TN, NT, (ABL & 32768) != 0>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv);
   } else {
     h3_epilogue16<BM, BN, WM, BN, TM, TN, NT, EPI, false>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
   }
@@ -559,7 +595,8 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
 
 template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int ABL = 0>
 inline int launch_conv_r3_cfg(const ConvArgs& a, hipStream_t st) {
-  if (!a.wh || !a.winv || a.Kpad % 32 != 0 || (a.nseg == 2 && a.kseg1 % 32 != 0) || a.N % BN != 0 || a.res_up) {
+  if (!a.wh || !a.winv || a.Kpad % 32 != 0 || (a.nseg == 2 && a.kseg1 % 32 != 0) || a.N % BN != 0 ||
+      (a.res_up && ((ABL & 32768) == 0 || (ABL & 2048) == 0 || a.res || a.nseg != 1))) {
     set_error("conv_r3: K/N not aligned to the tile, no split weights or an upsampled residual (Kpad=%d kseg1=%d N=%d)", a.Kpad,
               a.kseg1, a.N);
     return SFA_E_UNSUPPORTED;
