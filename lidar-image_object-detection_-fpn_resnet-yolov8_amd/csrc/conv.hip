@@ -64,7 +64,8 @@ static bool strip_ok(const ConvArgs& a) {
 //    downsample segments); on layer3/4 shapes it does not beat the strip / conv_h3 kernels. The
 //    strip kernel runs in the transposed-accumulator form too (float4 epilogue: -7..11 %;
 //    profiles/r02_convbench_*.txt). SFA_TUNE bits 4 / 8 / 16 return the heads / the big-M
-//    non-strip convs / the strip convs to the round-1 kernels for same-box A/B;
+//    non-strip convs / the strip convs to the round-1 kernels for same-box A/B, bit 32 the FPN
+//    skip convs, bit 64 the heads to the unpacked epilogue;
 //  * split-K 2 for the 512-wide (layer4) convs, whose 184 tiles cannot fill 256 CUs (-13..16 %);
 //    picked from the width only, so a frame's arithmetic never depends on the batch.
 // conv_x6g_kernel<..., PREC 1> tiles as the fallback.
@@ -81,7 +82,8 @@ static int tune_flags() {
 // for the second half of the waves (4).
 constexpr int R3_BODY = 256 | 2048;
 constexpr int R3_FPN = 256 | 2048 | 32768;  // + the upsampled-residual epilogue (FPN skip convs)
-constexpr int R3_HEAD = 256 | 2048 | 4 | 4096 | 8192 | 16384;  // + v_fma_mix split, 3-block W read-ahead, scalar tap decode
+constexpr int R3_HEAD = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536;  // + v_fma_mix split, 3-block W read-ahead,
+                                                                        // scalar tap decode, packed epilogue
 
 static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;
@@ -91,7 +93,10 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   const bool strip = strip_ok(a) && !sliced;
   if (epilogue == EPI_HEAD) {
     if (a.N == 320) {
-      if (!(tune_flags() & 4)) rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD>(a, st);
+      if (tune_flags() & 64)  // the unpacked head epilogue (A/B)
+        rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD & ~65536>(a, st);
+      else if (!(tune_flags() & 4))
+        rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD>(a, st);
       if (!ok(rc)) rc = launch_conv_h3_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2, 1>(a, st);
       if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 320, 32, EPI_HEAD, 1, 16, 3, 0, 320, 1>(a, st);
     }

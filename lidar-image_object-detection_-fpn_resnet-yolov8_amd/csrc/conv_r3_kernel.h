@@ -119,7 +119,7 @@ __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&ac
 // of both pixels (6 swaps + 6 adds, all VALU, no LDS, no barrier per head). The per-channel
 // weight scale winv = 2^-e (fp16x3) is folded into the staged 1x1 weights and biases
 // (w1 * winv, b / winv: exact power-of-two scalings), so T = max(acc * ainv + b', 0).
-template <int TM, int TN, int NT, int HPB>
+template <int TM, int TN, int NT, int HPB, bool PK = false>
 __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
                                                   int mrow0, int n0, int nt, int tid, const float (&ainv)[TM]) {
   static_assert(TM == 2, "pairwise swap reduction assumes two 16-row sub-tiles per wave");
@@ -151,6 +151,48 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
         hoff = a.hoff[j];
       }
     float p[TM][4];
+    if constexpr (PK) {
+      // packed form: the activations t of a (column block, channel pair) as one float2, so the
+      // bias fma and the 1x1 products run as v_pk_fma_f32 (2 lanes of work per VALU issue), and
+      // only the head's ch outputs are formed (ch is wave-uniform: a scalar branch per output)
+      using f2 = float __attribute__((ext_vector_type(2)));
+      f2 T[TM][4][2];
+#pragma unroll
+      for (int ci = 0; ci < 4; ++ci) {
+        const int ni = 4 * hh + ci;
+        const x6_f32x4 bp = *reinterpret_cast<const x6_f32x4*>(BP + hh * 64 + 16 * ci + 4 * g);
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const f2 r = __builtin_elementwise_fma(f2{acc[mi][ni][2 * h], acc[mi][ni][2 * h + 1]},
+                                                   f2{ainv[mi], ainv[mi]}, f2{bp[2 * h], bp[2 * h + 1]});
+            T[mi][ci][h] = __builtin_elementwise_max(r, f2{0.f, 0.f});
+          }
+      }
+#pragma unroll
+      for (int o = 0; o < 4; ++o) {
+        if (o < ch) {
+          f2 q[TM];
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi) q[mi] = f2{0.f, 0.f};
+#pragma unroll
+          for (int ci = 0; ci < 4; ++ci) {
+            const x6_f32x4 w = *reinterpret_cast<const x6_f32x4*>(WH + hh * 256 + o * 64 + 16 * ci + 4 * g);
+#pragma unroll
+            for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+              for (int h = 0; h < 2; ++h)
+                q[mi] = __builtin_elementwise_fma(T[mi][ci][h], f2{w[2 * h], w[2 * h + 1]}, q[mi]);
+          }
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi) p[mi][o] = q[mi].x + q[mi].y;
+        } else {
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi) p[mi][o] = 0.f;
+        }
+      }
+    } else {
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
@@ -171,6 +213,7 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
 #pragma unroll
           for (int o = 0; o < 4; ++o) p[mi][o] = fmaf(t, w[o][v], p[mi][o]);
         }
+    }
     }
     // level 1 (l ^ 32): lanes g < 2 keep outputs 0, 1, lanes g >= 2 outputs 2, 3
     swap_add32(p[0][0], p[0][2]);
@@ -196,6 +239,8 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
 // 32 = pure MFMA stream (no loads, split, W reads or barriers in the K loop: the ceiling),
 // 64 = no split in the K loop (A loads kept live), 128 = no barrier in the K loop (ablations),
 // 1024 = no epilogue (accumulators kept live; ablation of the epilogue cost),
+// 65536 = (heads, with 2048) packed epilogue: v_pk_fma_f32 over channel pairs, only the head's
+// ch outputs formed,
 // 32768 = (with 2048) the epilogue also takes an upsampled half-resolution residual (a.res_up:
 // the FPN skip convs; only those instances carry its registers),
 // 16384 = scalar tap decode + per-lane tap validity masks for the A addresses (one segment,
@@ -585,7 +630,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   __syncthreads();
   if constexpr ((ABL & 2048) != 0) {
     if constexpr (EPI == EPI_HEAD)
-      r3t_epilogue_head<TM, TN, NT, BN / 64>(a, acc, smem, m0 + wave * WM, n0, nt, tid, ainv);
+      r3t_epilogue_head<TM, TN, NT, BN / 64, (ABL & 65536) != 0>(a, acc, smem, m0 + wave * WM, n0, nt, tid, ainv);
     else
       r3t_epilogue_std<TM, TN, NT, (ABL & 32768) != 0>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv);
   } else {

@@ -263,7 +263,7 @@ int main(int argc, char** argv) {
       CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2),
   };
   std::vector<Cand> heads = {
-      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 14596, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 30980, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 30980, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 96516, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
