@@ -116,13 +116,12 @@ __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&ac
 // the head's 64 channels and the 1x1 conv's partial sums over them (4 outputs x TM pixels),
 // reduced over the pixel's four lanes (l, l ^ 16, l ^ 32, l ^ 48) by v_permlane32/16_swap: each
 // swap exchanges half of a pair of partials, so two levels leave lane l >> 4 = o with output o
-// of both pixels (6 swaps + 6 adds, all VALU, no LDS, no barrier per head). The per-channel
+// of each of its pixels (3 swaps + 3 adds per sub-tile, all VALU, no LDS, no barrier per head). The per-channel
 // weight scale winv = 2^-e (fp16x3) is folded into the staged 1x1 weights and biases
 // (w1 * winv, b / winv: exact power-of-two scalings), so T = max(acc * ainv + b', 0).
 template <int TM, int TN, int NT, int HPB, bool PK = false>
 __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
                                                   int mrow0, int n0, int nt, int tid, const float (&ainv)[TM]) {
-  static_assert(TM == 2, "pairwise swap reduction assumes two 16-row sub-tiles per wave");
   const int M = a.M, lane = tid & 63, c16 = lane & 15, g = lane >> 4;
   float* WH = reinterpret_cast<float*>(smem);  // [HPB][4][64]: w1 * winv
   float* BP = WH + HPB * 256;                  // [HPB * 64]: bias / winv
@@ -216,13 +215,14 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
     }
     }
     // level 1 (l ^ 32): lanes g < 2 keep outputs 0, 1, lanes g >= 2 outputs 2, 3
-    swap_add32(p[0][0], p[0][2]);
-    swap_add32(p[0][1], p[0][3]);
-    swap_add32(p[1][0], p[1][2]);
-    swap_add32(p[1][1], p[1][3]);
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      swap_add32(p[mi][0], p[mi][2]);
+      swap_add32(p[mi][1], p[mi][3]);
+    }
     // level 2 (l ^ 16): even rows keep the first of each pair, odd rows the second -> lane g: output g
-    swap_add16(p[0][0], p[0][1]);
-    swap_add16(p[1][0], p[1][1]);
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) swap_add16(p[mi][0], p[mi][1]);
     const float hb = a.hb1[head * 4 + g];
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
@@ -239,6 +239,7 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
 // 32 = pure MFMA stream (no loads, split, W reads or barriers in the K loop: the ceiling),
 // 64 = no split in the K loop (A loads kept live), 128 = no barrier in the K loop (ablations),
 // 1024 = no epilogue (accumulators kept live; ablation of the epilogue cost),
+// 131072 = no A loads in the K loop (with 256; ablation of the A-operand cost),
 // 65536 = (heads, with 2048) packed epilogue: v_pk_fma_f32 over channel pairs, only the head's
 // ch outputs formed,
 // 32768 = (with 2048) the epilogue also takes an upsampled half-resolution residual (a.res_up:
@@ -506,7 +507,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
         constexpr int SLOTS = (TN - 2) / 2 >= 1 ? (TN - 2) / 2 : 1;
         constexpr int PPB = (NB + SLOTS - 1) / SLOTS;
         static_assert(TN >= 4, "spread DMA needs 4 column blocks");
-        if (ni == 0 && more_a) load_a(kt0 + kt + 1);
+        if (ni == 0 && more_a && !(ABL & 131072)) load_a(kt0 + kt + 1);
         if (ni >= 2 && ((ni - 2) >> 1) * PPB < NB && more_w && !(ABL & 1) && wave_half == (ni & 1)) {
 #pragma unroll
           for (int jj = 0; jj < PPB; ++jj) {

@@ -1,6 +1,8 @@
 // Micro-benchmark of conv_mfma_kernel tile configurations on the KFPN layer
 // shapes at bs=16, 608x608 (tools only; not part of the product library).
-//   hipcc -O3 -std=c++17 --offload-arch=gfx950 tools/convbench.hip -o tools/convbench
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -pthread tools/convbench.hip -o tools/convbench
+//   ./tools/convbench [iters] [shape substring]; env SUSTAIN=<s>: also back-to-back for s seconds
+//   per candidate with the board's clock and power read mid-run (rocm-smi)
 //   ./tools/convbench [iters]
 // Every candidate's output is compared with the first candidate's (same math,
 // different tiling -> differences only from summation order).
@@ -12,6 +14,8 @@
 #include <functional>
 #include <string>
 #include <vector>
+#include <chrono>
+#include <thread>
 
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_x6_kernel.h"
@@ -236,6 +240,7 @@ static const size_t g_part_floats = 64u << 20;
 int main(int argc, char** argv) {
   const int iters = argc > 1 ? atoi(argv[1]) : 20;
   const char* only = argc > 2 ? argv[2] : nullptr;
+  const double sustain = getenv("SUSTAIN") ? atof(getenv("SUSTAIN")) : 0.0;
   std::vector<Shape> shapes = {
       {"stem 7x7/2 4->64", 16, 608, 608, 4, 7, 2, 3, 64, false, false},
       {"layer1 3x3 64->64 +res", 16, 152, 152, 64, 3, 1, 1, 64, false, true},
@@ -251,19 +256,18 @@ int main(int argc, char** argv) {
   };
   // round 2: conv_r3_kernel (A in registers) against the round-1 defaults (first entry of each)
   std::vector<Cand> n64 = {
-      CANDTA(128, 64, 32, EPI_STD, 3, 14), CANDTA(128, 64, 32, EPI_STD, 3, 30),
+      CANDTA(128, 64, 32, EPI_STD, 3, 14),
   };
   std::vector<Cand> stem = {
       CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
   };
   std::vector<Cand> nbig = {
       CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDR(128, 128, 32, EPI_STD, 2, 2, 2304, 1),
-      CANDR(128, 128, 32, EPI_STD, 3, 2, 2304, 1), CANDR(128, 64, 32, EPI_STD, 3, 2, 2304, 1),
-      CANDTA(128, 64, 32, EPI_STD, 3, 10), CANDTK(128, 128, 32, EPI_STD, 2, 10, 2),
       CANDN(128, 128, 32, EPI_STD, 2, 32, 2, false, 2),
   };
   std::vector<Cand> heads = {
-      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 30980, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 96516, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 96516, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 227588, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 96517, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 227589, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -392,6 +396,37 @@ int main(int argc, char** argv) {
       const float med = ms[ms.size() / 2];
       printf("  %-32s %9.1f us  %7.1f TF/s  maxdiff %.2e (|ref| %.2e)\n", c.name.c_str(), med * 1e3,
              flop / (med * 1e-3) / 1e12, maxd, maxr);
+      if (sustain > 0) {  // back-to-back launches for `sustain` s (board at its power limit)
+        std::string smi;
+        std::thread probe([&] {
+          std::this_thread::sleep_for(std::chrono::milliseconds((int)(sustain * 600)));
+          FILE* f = popen("rocm-smi --showpower --showclocks 2>/dev/null | grep -E 'sclk|Power \\(W\\)'", "r");
+          if (!f) return;
+          char buf[256];
+          while (fgets(buf, sizeof buf, f)) {
+            std::string l(buf);
+            const size_t k = l.find_last_of(':');
+            smi += (k == std::string::npos ? l : l.substr(k + 1));
+          }
+          pclose(f);
+          for (char& ch : smi)
+            if (ch == '\n' || ch == '\t') ch = ' ';
+        });
+        int n = 0;
+        float tot = 0;
+        CK(hipEventRecord(e0, st));
+        while (tot < sustain * 1000) {
+          for (int k = 0; k < 20; ++k) c.fn(a, st);
+          n += 20;
+          CK(hipEventRecord(e1, st));
+          CK(hipEventSynchronize(e1));
+          CK(hipEventElapsedTime(&tot, e0, e1));
+        }
+        probe.join();
+        const double per = tot / n;
+        printf("  %-32s sustained %.1f us  %7.1f TF/s  [smi:%s]\n", "", per * 1e3, flop / (per * 1e-3) / 1e12,
+               smi.c_str());
+      }
       if (wv != w) CK(hipFree(wv));
       if (a.wx) CK(hipFree(const_cast<uint16_t*>(a.wx)));
       if (whp) CK(hipFree(whp));
