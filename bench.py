@@ -44,6 +44,11 @@ PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA
 PEAK_BF16X6_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
 # fp16x3: 3 fp16 MFMA products per f32 MAC (fp16 MFMA has the bf16 rate)
 PEAK_FP16X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 3
+# measured on MI355X: pure v_mfma_f32_16x16x32_f16 chains over the whole chip settle at the
+# board's power / current limit (~1,990 MHz, 1,300 W): tools/micro/mfma_power.hip,
+# profiles/r02_power_cap.txt. The practical ceiling the bench (itself at the 1,375 W limit) sees.
+MEASURED_FP16_MFMA_CAPPED_TFLOPS = 1883.0
+PEAKS_CAPPED = {"fp16x3": MEASURED_FP16_MFMA_CAPPED_TFLOPS / 3, "bf16x6": MEASURED_FP16_MFMA_CAPPED_TFLOPS / 6}
 MATHS = {"fp16x3": _lib.MATH_FP16X3, "bf16x6": _lib.MATH_BF16X6, "f32": _lib.MATH_F32}
 PEAKS = {"fp16x3": (PEAK_FP16X3_TFLOPS, "dense fp16 MFMA 2500 TF / 3 fp16 products per f32 MAC"),
          "bf16x6": (PEAK_BF16X6_TFLOPS, "dense bf16 MFMA 2500 TF / 6 bf16 products per f32 MAC"),
@@ -456,6 +461,11 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4),
                 "frac_of_f32_mfma_peak": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
+                "peak_power_capped": (round(PEAKS_CAPPED[args.math], 2) if args.math in PEAKS_CAPPED else None),
+                "frac_of_power_capped": (round(achieved / PEAKS_CAPPED[args.math], 4)
+                                         if args.math in PEAKS_CAPPED else None),
+                "peak_power_capped_basis": "measured pure-MFMA chip ceiling at the board power limit "
+                                           "(1883 TF fp16 / products per MAC; profiles/r02_power_cap.txt)",
                 "traffic": traffic_per_forward(args),
                 "algorithmic_flop_per_step": flop_step,
             },
