@@ -65,7 +65,8 @@ static bool strip_ok(const ConvArgs& a) {
 //    strip kernel runs in the transposed-accumulator form too (float4 epilogue: -7..11 %;
 //    profiles/r02_convbench_*.txt). SFA_TUNE bits 4 / 8 / 16 return the heads / the big-M
 //    non-strip convs / the strip convs to the round-1 kernels for same-box A/B, bit 32 the FPN
-//    skip convs, bit 64 the heads to the unpacked epilogue;
+//    skip convs, bit 64 the heads to the unpacked epilogue, bit 128 the 64-wide strip convs to
+//    no residual prefetch;
 //  * split-K 2 for the 512-wide (layer4) convs, whose 184 tiles cannot fill 256 CUs (-13..16 %);
 //    picked from the width only, so a frame's arithmetic never depends on the batch.
 // conv_x6g_kernel<..., PREC 1> tiles as the fallback.
@@ -82,6 +83,12 @@ static int tune_flags() {
 // for the second half of the waves (4).
 constexpr int R3_BODY = 256 | 2048;
 constexpr int R3_FPN = 256 | 2048 | 32768;  // + the upsampled-residual epilogue (FPN skip convs)
+// strip kernel (conv_h3s_kernel.h ABL bits): transposed epilogue (2), v_fma_mix split (8); the
+// 64-wide also pre-split strip (4) and the residual tile loaded during the last super-step (128).
+// Non-temporal output stores (strip 2048, r3 262144) are 1-6 % faster per launch in isolation but
+// 1.2 % slower end to end (the next conv then reads its input from HBM): not used.
+constexpr int H3S_64 = 2 | 4 | 8 | 128;
+constexpr int H3S_128 = 2 | 8;
 constexpr int R3_HEAD = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536;  // + v_fma_mix split, 3-block W read-ahead,
                                                                         // scalar tap decode, packed epilogue
 
@@ -114,7 +121,8 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     if (strip) {
       if (tune_flags() & 16) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3>(a, st);
       else if (tune_flags() & 1) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 2>(a, st);
-      else rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 14>(a, st);  // + pre-split strip, v_fma_mix split
+      else if (tune_flags() & 128) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 14>(a, st);  // round-2 A/B
+      else rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, H3S_64>(a, st);
     }
     if (!ok(rc) && a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 64, 32, EPI_STD, 2, 16, 3, false, 0>(a, st);
@@ -129,7 +137,7 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
         rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
       else if (tune_flags() & 2)
         rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3, 10>(b, st);
-      if (!ok(rc)) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, 10>(b, st);  // transposed, v_fma_mix split
+      if (!ok(rc)) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, H3S_128>(b, st);
     } else if (tile_rows(a) >= 50000 && !(tune_flags() & 8)) {  // big-M stride-2 / two-segment: A from registers
       rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
     }

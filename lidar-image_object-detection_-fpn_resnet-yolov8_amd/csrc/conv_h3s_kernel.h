@@ -21,6 +21,11 @@
 namespace sfa {
 
 // ABL: 1 = no fp16x3 split (the f32 bits are fed to the MFMAs; convbench ablation only),
+// 32 = no epilogue, 64 = no pre-split VALU (ablations, results wrong), 128 = (with 4 and 2) the
+// residual tile loaded at the last super-step's kw 1 (in place of the no-op strip reload), so
+// the last six k-steps' MFMAs hide its latency, 256 / 512 = epilogue without stores / without
+// the amax record (ablations), 1024 = (with 2) output tile staged in LDS and stored
+// row-contiguous (whole 128-B lines per store instruction), 2048 = non-temporal output stores,
 // 2 = transposed accumulators (W fragment as the MFMA A operand) with conv_r3_kernel.h's float4
 // epilogue (r3t_epilogue_std) and float4 split-K partials,
 // 4 = pre-split strip: at kw 0 each wave splits ITS rows of the f32 strip (WM + 2 rows, the kw
@@ -45,11 +50,15 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
   constexpr int NB = (ND_B + NW - 1) / NW, NB_REM = ND_B % NW;
   constexpr int HEAD_BYTES = EPI == EPI_HEAD ? BM * 65 * 4 + (BN / 64) * 1024 : 0;  // h3_epilogue16
   constexpr bool PS = (ABL & 4) != 0;
+  constexpr bool RESPF = PS && (ABL & 128) != 0 && (ABL & 2) != 0 && (ABL & 16) == 0;
   constexpr int PROWS = WM + 2;              // a wave's pre-split rows (its WM rows + the kw halo)
   constexpr int PR_BYTES = (PROWS + 1) * 64;  // per term: 32 fp16 per row, + one zero row
   constexpr int NSB = PS ? 1 : 2;             // f32 strip buffers
   constexpr int MAIN_BYTES = NSB * S_BYTES + 2 * W_BYTES + (PS ? NW * 2 * PR_BYTES : 0);
-  constexpr int LDS_BYTES = MAIN_BYTES > HEAD_BYTES ? MAIN_BYTES : HEAD_BYTES;
+  constexpr bool STG = (ABL & 1024) != 0 && (ABL & 2) != 0 && EPI == EPI_STD;  // row-contiguous stores via LDS
+  constexpr int STG_BYTES = STG ? r3t_stage_bytes<TM, TN, NT>() : 0;
+  constexpr int LDS_BYTES0 = MAIN_BYTES > HEAD_BYTES ? MAIN_BYTES : HEAD_BYTES;
+  constexpr int LDS_BYTES = LDS_BYTES0 > STG_BYTES ? LDS_BYTES0 : STG_BYTES;
   static_assert(NW % 2 == 0 && WM % 16 == 0 && BN % 16 == 0, "tile");
   static_assert((ABL & 2) == 0 || EPI == EPI_STD, "transposed form: standard epilogue only");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
@@ -175,6 +184,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     for (int ni = 0; ni < TN; ++ni)
 #pragma unroll
       for (int v = 0; v < 4; ++v) acc[mi][ni][v] = 0.f;
+  x6_f32x4 rvp[TM][TN];  // RESPF: the residual tile, loaded during the last super-step
 
   unsigned char* const PH = smem + NSB * S_BYTES + 2 * W_BYTES + wave * 2 * PR_BYTES;  // PS: hi rows, lo + PR_BYTES
   auto presplit = [&](const unsigned char* Ss) {
@@ -187,7 +197,12 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
         const x6_f32x4 x = *reinterpret_cast<const x6_f32x4*>(Ss + j * AROW + ((q ^ swzA(j)) << 4));
         const float sc = m0 - 1 + j >= fb ? sB : sA;
         const int off = r * 64 + (((q >> 1) ^ swzP(r)) << 4) + (q & 1) * 8;
-        if constexpr ((ABL & 8) != 0) {
+        if constexpr ((ABL & 64) != 0) {  // ablation: no split VALU (raw bits stored)
+          typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+          const u32x2_t raw = u32x2_t{__float_as_uint(x[0]) ^ __float_as_uint(x[1]), __float_as_uint(x[2])};
+          *reinterpret_cast<u32x2_t*>(PH + off) = raw;
+          *reinterpret_cast<u32x2_t*>(PH + PR_BYTES + off) = raw;
+        } else if constexpr ((ABL & 8) != 0) {
           typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
           unsigned h0, h1, l0, l1;
           split2h_pair(x[0], x[1], sc, h0, l0);
@@ -302,7 +317,12 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
       if constexpr (PS) {
         // kw 2: W(t) landed (the next strip, issued after it at kw 1, may still fly); else all
         if (kw == 2) {
-          if (NS_REM == 0 || wave < NS_REM)
+          if (RESPF && last) {  // the residual loads issued at kw 1 may still fly
+            if (a.res && nsplit == 1)
+              asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TM * TN) : "memory");
+            else
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          } else if (NS_REM == 0 || wave < NS_REM)
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS) : "memory");
           else
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS - 1) : "memory");
@@ -314,7 +334,13 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
         unsigned char* const wdst = WB + ((t + 1) & 1) * W_BYTES;
         if constexpr (!SPREAD) {
           load_w(wnext, wdst);
-          if (kw == 1) load_strip(last ? s : s + 1, smem);  // every wave has split strip s
+          if (kw == 1) {
+            if (RESPF && last) {  // the residual tile (the last MFMAs hide its latency)
+              if (a.res && nsplit == 1) r3t_res_load<TM, TN>(a, rvp, m0 + wave * WM, n0, lane);
+            } else {
+              load_strip(last ? s : s + 1, smem);  // every wave has split strip s
+            }
+          }
         }
         if (kw == 0) presplit(smem);
         compute(smem, WB + (t & 1) * W_BYTES, kw, [&](int ni) {
@@ -374,9 +400,17 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
         }
     return;
   }
+  if constexpr ((ABL & 32) != 0) {  // ablation: no epilogue (accumulators kept live)
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) asm volatile("" ::"v"(acc[mi][ni]));
+    return;
+  }
   __syncthreads();
   if constexpr ((ABL & 2) != 0 && EPI == EPI_STD)
-    r3t_epilogue_std<TM, TN, NT>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv);
+    r3t_epilogue_std<TM, TN, NT, false, RESPF, ((ABL >> 8) & 3) | ((ABL >> 9) & 4), STG>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv,
+                                                                    rvp);
   else
     h3_epilogue16<BM, BN, WM, BN, TM, TN, NT, EPI, false>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
 }

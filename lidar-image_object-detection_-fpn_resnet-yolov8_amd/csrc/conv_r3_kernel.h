@@ -40,15 +40,40 @@ typedef unsigned r3_u32x4 __attribute__((ext_vector_type(4)));
 // RU: the residual may also be given at half resolution (a.res_up, the FPN skip convs), added
 // bilinearly upsampled x2 (align_corners) exactly as res_up_sample evaluates it, 4 float4 taps
 // per lane and column block (the 4 channels of the lane).
-template <int TM, int TN, int NT, bool RU = false>
+// The residual tile of r3t_epilogue_std in the transposed layout (lane: 4 channels of one row),
+// loaded ahead of the epilogue by callers that can hide its latency behind their last MFMAs.
+template <int TM, int TN>
+__device__ __forceinline__ void r3t_res_load(const ConvArgs& a, x6_f32x4 (&rv)[TM][TN], int mrow0, int n0, int lane) {
+  const int c16 = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      const int m = min(mrow0 + mi * 16 + c16, a.M - 1);
+      rv[mi][ni] = *reinterpret_cast<const x6_f32x4*>(a.res + (size_t)m * a.N + n0 + ni * 16 + 4 * g);
+    }
+}
+
+// STG: the wave's output tile (WM rows x BN channels) is staged in LDS (row pitch BN * 4 + 16 B:
+// conflict-free float4 writes and reads) and stored row-contiguous: each store instruction then
+// writes 64 x 16 B = whole 128-B lines (BN / 4 lanes per row) instead of 16 rows x 64 B halves.
+template <int TM, int TN, int NT>
+constexpr int r3t_stage_bytes() {
+  return (NT / 64) * (TM * 16) * (TN * 64 + 16) + 2 * (NT / 64) * 4;
+}
+
+template <int TM, int TN, int NT, bool RU = false, bool PRE = false, int EABL = 0, bool STG = false>
 __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
-                                                 int mrow0, int m0, int n0, int lane, const float (&ainv)[TM]) {
+                                                 int mrow0, int m0, int n0, int lane, const float (&ainv)[TM],
+                                                 const x6_f32x4 (*pre)[TN] = nullptr) {
   // every element is evaluated by the same rounding sequence (explicit fmaf, no contraction):
   // left to the compiler, the unrolled copies were contracted differently (some mul + add, some
   // fma, some packed), so a pixel's value depended on its row within the tile, i.e. on the
   // batch it was computed in
 #pragma clang fp contract(off)
   const int M = a.M, c16 = lane & 15, g = lane >> 4;
+  constexpr int PITCH = TN * 64 + 16;  // STG: bytes per staged row
+  unsigned char* const stg = smem + (threadIdx.x >> 6) * (TM * 16) * PITCH;
   AmaxRows am(a.OH * a.OW, m0);
   x6_f32x4 rv[TM][TN];
   if (RU && a.res_up) {
@@ -78,13 +103,14 @@ __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&ac
     }
   }
   if (a.res) {
+    if constexpr (PRE) {  // loaded by the caller (r3t_res_load)
 #pragma unroll
-    for (int mi = 0; mi < TM; ++mi)
+      for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < TN; ++ni) {
-        const int m = min(mrow0 + mi * 16 + c16, M - 1);
-        rv[mi][ni] = *reinterpret_cast<const x6_f32x4*>(a.res + (size_t)m * a.N + n0 + ni * 16 + 4 * g);
-      }
+        for (int ni = 0; ni < TN; ++ni) rv[mi][ni] = pre[mi][ni];
+    } else {
+      r3t_res_load<TM, TN>(a, rv, mrow0, n0, lane);
+    }
   }
 #pragma unroll
   for (int ni = 0; ni < TN; ++ni) {
@@ -102,14 +128,39 @@ __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&ac
         if (a.relu) t = fmaxf(t, 0.f);
         val[v] = t;
       }
-      if (m < M) {
-        *reinterpret_cast<x6_f32x4*>(a.y + (size_t)m * a.N + n) = val;
-        if (a.amax_out)
+      if constexpr (STG) {
+        *reinterpret_cast<x6_f32x4*>(stg + (mi * 16 + c16) * PITCH + (ni * 16 + 4 * g) * 4) = val;
+        if (m < M && a.amax_out && (EABL & 2) == 0)
+          am.add(a.amax_out, m, fmaxf(fmaxf(fabsf(val[0]), fabsf(val[1])), fmaxf(fabsf(val[2]), fabsf(val[3]))));
+      } else if (m < M) {
+        if constexpr ((EABL & 4) != 0)  // streaming (non-temporal) store
+          __builtin_nontemporal_store(val, reinterpret_cast<x6_f32x4*>(a.y + (size_t)m * a.N + n));
+        else if constexpr ((EABL & 1) == 0) *reinterpret_cast<x6_f32x4*>(a.y + (size_t)m * a.N + n) = val;
+        else asm volatile("" ::"v"(val));
+        if (a.amax_out && (EABL & 2) == 0)
           am.add(a.amax_out, m, fmaxf(fmaxf(fabsf(val[0]), fabsf(val[1])), fmaxf(fabsf(val[2]), fabsf(val[3]))));
       }
     }
   }
-  if (a.amax_out) amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1, reinterpret_cast<float*>(smem));
+  if constexpr (STG) {
+    // the wave's own rows only: its LDS writes are complete once lgkmcnt drains (no barrier)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    constexpr int LPR = TN * 4;        // lanes per row (16 B each)
+    constexpr int RPI = 64 / LPR;      // rows per store instruction
+    const int rr = lane / LPR, q = lane % LPR;
+#pragma unroll
+    for (int k = 0; k < TM * 16 / RPI; ++k) {
+      const int r = k * RPI + rr, m = mrow0 + r;
+      const x6_f32x4 v = *reinterpret_cast<const x6_f32x4*>(stg + r * PITCH + q * 16);
+      if (m < M) {
+        if constexpr ((EABL & 1) == 0) *reinterpret_cast<x6_f32x4*>(a.y + (size_t)m * a.N + n0 + 4 * q) = v;
+        else asm volatile("" ::"v"(v));
+      }
+    }
+  }
+  if (a.amax_out && (EABL & 2) == 0)
+    amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1,
+                               reinterpret_cast<float*>(smem + (STG ? (NT / 64) * (TM * 16) * PITCH : 0)));
 }
 
 // Heads (EPI_HEAD, transposed form): per head and pixel, ReLU(conv3x3 + b) of the lane's 16 of
@@ -239,6 +290,7 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
 // 32 = pure MFMA stream (no loads, split, W reads or barriers in the K loop: the ceiling),
 // 64 = no split in the K loop (A loads kept live), 128 = no barrier in the K loop (ablations),
 // 1024 = no epilogue (accumulators kept live; ablation of the epilogue cost),
+// 262144 = (with 2048, standard epilogue) non-temporal output stores,
 // 131072 = no A loads in the K loop (with 256; ablation of the A-operand cost),
 // 65536 = (heads, with 2048) packed epilogue: v_pk_fma_f32 over channel pairs, only the head's
 // ch outputs formed,
@@ -633,7 +685,8 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
     if constexpr (EPI == EPI_HEAD)
       r3t_epilogue_head<TM, TN, NT, BN / 64, (ABL & 65536) != 0>(a, acc, smem, m0 + wave * WM, n0, nt, tid, ainv);
     else
-      r3t_epilogue_std<TM, TN, NT, (ABL & 32768) != 0>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv);
+      r3t_epilogue_std<TM, TN, NT, (ABL & 32768) != 0, false, (ABL & 262144) ? 4 : 0>(a, acc, smem, m0 + wave * WM, m0, n0,
+                                                                                      lane, ainv);
   } else {
     h3_epilogue16<BM, BN, WM, BN, TM, TN, NT, EPI, false>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
   }

@@ -256,17 +256,13 @@ int main(int argc, char** argv) {
   };
   // round 2: conv_r3_kernel (A in registers) against the round-1 defaults (first entry of each)
   std::vector<Cand> n64 = {
-      CANDTA(128, 64, 32, EPI_STD, 3, 14), CANDTA(128, 64, 64, EPI_STD, 3, 14),
-      CANDTA(128, 64, 64, EPI_STD, 2, 14), CANDTA(256, 64, 64, EPI_STD, 1, 14),
+      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDTA(128, 64, 32, EPI_STD, 3, 2190),
   };
   std::vector<Cand> stem = {
       CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
   };
   std::vector<Cand> nbig = {
-      CANDTK(128, 128, 32, EPI_STD, 2, 10, 1), CANDTK(128, 128, 32, EPI_STD, 2, 10, 2),
-      CANDTK(64, 128, 16, EPI_STD, 3, 10, 1), CANDTK(64, 128, 16, EPI_STD, 3, 10, 2),
-      CANDTK(128, 64, 32, EPI_STD, 3, 10, 1), CANDTK(128, 64, 32, EPI_STD, 3, 10, 2),
-      CANDTK(128, 128, 32, EPI_STD, 2, 10, 4),
+      CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDTA(128, 128, 32, EPI_STD, 2, 2058),
   };
   std::vector<Cand> heads = {
       CANDR(256, 320, 32, EPI_HEAD, 1, 2, 96516, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 88324, 1),

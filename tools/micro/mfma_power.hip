@@ -13,9 +13,13 @@ typedef float f16v __attribute__((ext_vector_type(16)));
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
-template <int SHAPE>  // 0: 16x16x32, 1: 32x32x16
+template <int SHAPE, int NV = 0>  // 0: 16x16x32, 1: 32x32x16; NV: f32 FMAs (VALU) per MFMA (SHAPE 0)
 __global__ void __launch_bounds__(512, 1) mfma_loop(const h8* __restrict__ in, float* __restrict__ out, int iters) {
   const int lane = threadIdx.x & 63;
+  float vq[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) vq[i] = (float)in[lane * 8 + i][0];
+  const float vm = (float)in[lane][1], va = (float)in[lane][2];
   h8 a[4], b[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -30,9 +34,18 @@ __global__ void __launch_bounds__(512, 1) mfma_loop(const h8* __restrict__ in, f
 #pragma unroll
       for (int i = 0; i < 16; ++i) c[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i & 3], b[i >> 2], c[i], 0, 0, 0);
 #pragma unroll
-      for (int i = 0; i < 16; ++i) c[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[(i + 1) & 3], b[i >> 2], c[i], 0, 0, 0);
+      for (int i = 0; i < 16; ++i) {
+        c[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[(i + 1) & 3], b[i >> 2], c[i], 0, 0, 0);
+        if constexpr (NV > 0) {
+#pragma unroll
+          for (int v = 0; v < NV; ++v)  // one VALU instruction each (no packing)
+            asm volatile("v_fma_f32 %0, %0, %1, %2" : "+v"(vq[(i * NV + v) & 7]) : "v"(vm), "v"(va));
+        }
+      }
     }
     float s = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += vq[i];
 #pragma unroll
     for (int i = 0; i < 16; ++i) s += c[i][0] + c[i][1] + c[i][2] + c[i][3];
     out[blockIdx.x * 512 + threadIdx.x] = s;
@@ -73,23 +86,27 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   const double flop = (double)blocks * 8 * iters * 32 * 16384;  // per launch
-  for (int shape = 0; shape < 2; ++shape) {
-    for (int rep = 0; rep < 2; ++rep) {
+  const char* names[5] = {"16x16x32", "32x32x16", "16x16x32 +0.5 VALU/MFMA", "16x16x32 +1 VALU/MFMA",
+                          "16x16x32 +2 VALU/MFMA"};
+  for (int shape = 0; shape < 5; ++shape) {
+    for (int rep = 0; rep < 1 + (shape < 2); ++rep) {
       int launches = 0;
       float total_ms = 0;
       CK(hipEventRecord(e0));
       while (total_ms < secs * 1000) {
         for (int k = 0; k < 20; ++k) {
           if (shape == 0) mfma_loop<0><<<blocks, 512>>>(in, out, iters);
-          else mfma_loop<1><<<blocks, 512>>>(in, out, iters);
+          else if (shape == 1) mfma_loop<1><<<blocks, 512>>>(in, out, iters);
+          else if (shape == 2) mfma_loop<0, 1><<<blocks, 512>>>(in, out, iters);
+          else if (shape == 3) mfma_loop<0, 2><<<blocks, 512>>>(in, out, iters);
+          else mfma_loop<0, 4><<<blocks, 512>>>(in, out, iters);
         }
         launches += 20;
         CK(hipEventRecord(e1));
         CK(hipEventSynchronize(e1));
         CK(hipEventElapsedTime(&total_ms, e0, e1));
       }
-      printf("%s rep %d: %.1f TFLOP/s dense fp16 over %.2f s (%d launches)\n",
-             shape == 0 ? "16x16x32" : "32x32x16", rep, flop * launches / (total_ms * 1e-3) / 1e12, total_ms * 1e-3,
+      printf("%s rep %d: %.1f TFLOP/s dense fp16 over %.2f s (%d launches)\n", names[shape], rep, flop * launches / (total_ms * 1e-3) / 1e12, total_ms * 1e-3,
              launches);
       fflush(stdout);
     }
