@@ -82,6 +82,12 @@ def parse():
                     help="steps in flight on separate streams (each with its own buffers and "
                          "model handle); >1 lets one step's kernel tails overlap the next's")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--serial-heads", action="store_true",
+                    help="keep the level-0 heads on the main stream (no side stream) for the whole "
+                         "run: with --inflight 1 every head launch then has the chip to itself, "
+                         "the configuration the roofline probe measures (for rocprof agreement)")
+    ap.add_argument("--probe-forwards", type=int, default=10,
+                    help="un-captured forwards timed per head launch for the roofline")
     ap.add_argument("--cpu-frames", type=int, default=4, help="frames timed for the CPU baseline")
     return ap.parse_args()
 
@@ -182,6 +188,71 @@ def traffic_per_forward(args):
         return None
     with open(files[-1]) as f:
         return int(json.load(f)["conv_hbm_bytes_per_forward"])
+
+
+def head_flop_per_launch(args):
+    """Algorithmic f32 FLOP of one head-level launch: the 5 heads' 3x3 convs
+    (C_l -> 64 each, as one N = 320 GEMM) + their 1x1 convs (64 -> c_h), over B frames."""
+    hc = sum(c for c in DEFAULT_HEADS.values())
+    n = 64 * len(DEFAULT_HEADS)
+    out = []
+    for c_in, div in ((256, 8), (128, 4), (64, 4)):
+        px = args.batch * (608 // div) ** 2
+        out.append(2 * px * (n * 9 * c_in + hc * 64))
+    return out
+
+
+def probe_heads(args, pipe, step):
+    """Per-launch durations of the dominant kernel (the fused detection heads, one launch per
+    KFPN level, 54.6 % of the FLOPs) from HIP events the library records on the launching
+    stream around each launch (sfa_model_set_probe): un-captured forwards, one step in flight,
+    all launches on one stream, so each head launch has the chip to itself."""
+    if args.workload != "bev_infer":
+        return None
+    eng = pipe.engine
+    eng.set_probe(_lib.PROBE_HEADS | _lib.PROBE_SERIAL)
+    try:
+        torch.cuda.synchronize()
+        per = []
+        for _ in range(args.probe_forwards):
+            step.fns[0]()
+            per.append(eng.probe_times(3))
+    finally:
+        eng.set_probe(_lib.PROBE_SERIAL if args.serial_heads else 0)
+    return np.median(np.array(per), axis=0).tolist()  # ms per level
+
+
+def roofline_line(args, heads, forward_roofline, fwd_achieved, peak, peak_basis, capped):
+    line = {"bound": "mfma", "unit": "TFLOP/s", "peak": round(peak, 2), "peak_basis": peak_basis,
+            "peak_power_capped": round(capped, 2) if capped else None,
+            "peak_power_capped_basis": "measured pure-MFMA chip ceiling at the board power limit "
+                                       "(1883 TF fp16 / products per MAC; profiles/r02_power_cap.txt)",
+            "traffic": None, "forward": forward_roofline}
+    fwd_traffic = traffic_per_forward(args)
+    forward_roofline["traffic"] = fwd_traffic
+    if heads is None:  # no probe: the whole forward is the unit
+        line.update({"kernel": "the whole forward (math %s)" % args.math, "achieved": round(fwd_achieved, 3),
+                     "frac": round(fwd_achieved / peak, 4), "traffic": fwd_traffic})
+        return line
+    flops = head_flop_per_launch(args)
+    ach = sum(flops) / (sum(heads) * 1e-3) / 1e12
+    line.update({
+        "kernel": {"fp16x3": "conv_r3_kernel<256, 320, ...> (fused detection heads: 3x3 conv C->5x64 + bias + "
+                             "ReLU + the 5 heads' 1x1 convs; one launch per KFPN level)",
+                   "bf16x6": "conv_x6g_kernel<256, 320, ...> (fused detection heads)",
+                   "f32": "conv_mfma_kernel<128, 64, ...> (detection heads)"}[args.math],
+        "achieved": round(ach, 3), "frac": round(ach / peak, 4),
+        "frac_of_power_capped": round(ach / capped, 4) if capped else None,
+        "frac_of_f32_mfma_peak": round(ach / PEAK_FP32_MFMA_TFLOPS, 4),
+        "measured": "HIP events on the launching stream around each head launch, median of %d "
+                    "un-captured forwards, one step in flight, no side stream (sfa_model_set_probe); "
+                    "achieved = algorithmic FLOP of the 3 launches / their summed durations" % args.probe_forwards,
+        "launch_us": [round(1e3 * v, 1) for v in heads],
+        "avg_launch_us": round(1e3 * sum(heads) / 3, 1),
+        "algorithmic_flop_per_launch": flops,
+        "traffic": None,
+    })
+    return line
 
 
 def cpu_baseline(args):
@@ -344,6 +415,9 @@ def main():
         return
     nf = max(1, args.inflight)
     pipes = [build_pipeline(dev, args, rank) for _ in range(nf)]
+    if args.serial_heads:
+        for p in pipes:
+            p.engine.set_probe(_lib.PROBE_SERIAL)
     steps = [StepGraphs(p, not args.no_graph) for p in pipes]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nf - 1)]
     gather = world > 1
@@ -405,6 +479,7 @@ def main():
         torch.cuda.synchronize()
     fwd_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
+    heads = probe_heads(args, pipes[0], steps[0]) if rank == 0 and args.probe_forwards > 0 else None
     if world > 1:
         t = torch.tensor([elapsed, fwd_ms, dec_ms], dtype=torch.float64,
                          device=dev if dist.get_backend() == "nccl" else "cpu")
@@ -417,6 +492,13 @@ def main():
         # the forward's own event time with one step in flight (the conv launches + aux)
         achieved = flop_step / (fwd_ms * 1e-3) / 1e12
         peak, peak_basis = PEAKS[args.math]
+        capped = PEAKS_CAPPED.get(args.math)
+        forward_roofline = {
+            "scope": "the whole forward (22 implicit-GEMM launches + the stem + aux kernels), "
+                     "algorithmic f32 FLOP over its event time with one step in flight",
+            "achieved": round(achieved, 3), "frac": round(achieved / peak, 4),
+            "frac_of_power_capped": round(achieved / capped, 4) if capped else None,
+            "algorithmic_flop_per_step": flop_step}
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -446,29 +528,7 @@ def main():
             },
             "stages_ms": {"forward": round(fwd_ms, 4), "decode": round(dec_ms, 4),
                           "note": "one step in flight; value/ms_per_step use %d in flight" % nf},
-            "roofline": {
-                "bound": "mfma",
-                "kernel": {"f32": "conv_mfma_kernel", "bf16x6": "conv_x6_kernel / conv_x6g_kernel",
-                           "fp16x3": "conv_r3_kernel (heads, 49 % of the conv time) / conv_h3s_kernel / "
-                                     "conv_h3_kernel"}.get(args.math, args.math) + " (math %s)" % args.math +
-                          (" (22 implicit-GEMM launches + the LDS-patch stem" if args.math == "fp16x3"
-                           else " (23 implicit-GEMM launches") +
-                          " per forward; achieved = algorithmic f32 FLOP "
-                          "over the whole forward's event time, aux kernels included)",
-                "achieved": round(achieved, 3),
-                "peak": round(peak, 2),
-                "peak_basis": peak_basis,
-                "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4),
-                "frac_of_f32_mfma_peak": round(achieved / PEAK_FP32_MFMA_TFLOPS, 4),
-                "peak_power_capped": (round(PEAKS_CAPPED[args.math], 2) if args.math in PEAKS_CAPPED else None),
-                "frac_of_power_capped": (round(achieved / PEAKS_CAPPED[args.math], 4)
-                                         if args.math in PEAKS_CAPPED else None),
-                "peak_power_capped_basis": "measured pure-MFMA chip ceiling at the board power limit "
-                                           "(1883 TF fp16 / products per MAC; profiles/r02_power_cap.txt)",
-                "traffic": traffic_per_forward(args),
-                "algorithmic_flop_per_step": flop_step,
-            },
+            "roofline": roofline_line(args, heads, forward_roofline, achieved, peak, peak_basis, capped),
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args)

@@ -138,6 +138,17 @@ enum sfa_math { SFA_MATH_F32 = 0, SFA_MATH_BF16X6 = 1, SFA_MATH_FP16X3 = 2 };
 int sfa_model_set_math(sfa_model* model, int math);
 int sfa_model_get_math(const sfa_model* model);
 
+/* Kernel probe (measurement only; no reference counterpart).  SFA_PROBE_HEADS: every
+ * forward NOT being captured into a graph records a timing event before and after each
+ * detection-head level's launch (the dominant kernel, 54.6 % of the FLOPs), on the stream
+ * that launches it; SFA_PROBE_SERIAL: all launches stay on the caller's stream (no
+ * level-0 side stream), so each head launch has the chip to itself.  sfa_model_probe_times
+ * waits for the last probed forward's events and returns the launch durations of head
+ * levels 0 .. n-1 in ms.  flags = 0 turns the probe off. */
+enum sfa_probe_flags { SFA_PROBE_HEADS = 1, SFA_PROBE_SERIAL = 2 };
+int sfa_model_set_probe(sfa_model* model, int flags);
+int sfa_model_probe_times(const sfa_model* model, float* ms, int n);
+
 /* Forward.  x: device float32, layout SFA_IN_NCHW3 (B,3,H,W) as the reference
  * takes it, SFA_IN_NHWC4 (B,H,W,4) as sfa_bev_voxelize writes it, or
  * SFA_IN_NCHW3_FLIP_HW: (B,3,H,W) read as torch.flip(x, [2, 3]) — the back view of

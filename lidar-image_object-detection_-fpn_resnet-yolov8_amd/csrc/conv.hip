@@ -66,7 +66,7 @@ static bool strip_ok(const ConvArgs& a) {
 //    profiles/r02_convbench_*.txt). SFA_TUNE bits 4 / 8 / 16 return the heads / the big-M
 //    non-strip convs / the strip convs to the round-1 kernels for same-box A/B, bit 32 the FPN
 //    skip convs, bit 64 the heads to the unpacked epilogue, bit 128 the 64-wide strip convs to
-//    no residual prefetch;
+//    no residual prefetch, bit 256 the conv_r3 launches to the tap-major K order;
 //  * split-K 2 for the 512-wide (layer4) convs, whose 184 tiles cannot fill 256 CUs (-13..16 %);
 //    picked from the width only, so a frame's arithmetic never depends on the batch.
 // conv_x6g_kernel<..., PREC 1> tiles as the fallback.
@@ -81,7 +81,9 @@ static int tune_flags() {
 // conv_r3_kernel variants (conv_r3_kernel.h ABL bits): W DMA spread over the column blocks (256),
 // transposed accumulators with float4 / permlane-swap epilogues (2048); heads also s_setprio 1
 // for the second half of the waves (4).
-constexpr int R3_BODY = 256 | 2048;
+// 524288: channel-chunk-major K order (the 3x3 window's 32-channel slices stay in L2 across the 9
+// taps; heads' HBM traffic 3.5-4.7x lower, -3..7 % per launch: profiles/r02_convbench_cmaj.txt)
+constexpr int R3_BODY = 256 | 2048 | 524288;
 constexpr int R3_FPN = 256 | 2048 | 32768;  // + the upsampled-residual epilogue (FPN skip convs)
 // strip kernel (conv_h3s_kernel.h ABL bits): transposed epilogue (2), v_fma_mix split (8); the
 // 64-wide also pre-split strip (4) and the residual tile loaded during the last super-step (128).
@@ -89,8 +91,9 @@ constexpr int R3_FPN = 256 | 2048 | 32768;  // + the upsampled-residual epilogue
 // 1.2 % slower end to end (the next conv then reads its input from HBM): not used.
 constexpr int H3S_64 = 2 | 4 | 8 | 128;
 constexpr int H3S_128 = 2 | 8;
-constexpr int R3_HEAD = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536;  // + v_fma_mix split, 3-block W read-ahead,
-                                                                        // scalar tap decode, packed epilogue
+constexpr int R3_HEAD = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536 | 524288;  // + v_fma_mix split, 3-block W
+                                                                                 // read-ahead, scalar tap decode,
+                                                                                 // packed epilogue, chunk-major K
 
 static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;
@@ -102,6 +105,8 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     if (a.N == 320) {
       if (tune_flags() & 64)  // the unpacked head epilogue (A/B)
         rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD & ~65536>(a, st);
+      else if (tune_flags() & 256)  // tap-major K order (A/B)
+        rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD & ~524288>(a, st);
       else if (!(tune_flags() & 4))
         rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD>(a, st);
       if (!ok(rc)) rc = launch_conv_h3_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2, 1>(a, st);
@@ -139,7 +144,10 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
         rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3, 10>(b, st);
       if (!ok(rc)) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, H3S_128>(b, st);
     } else if (tile_rows(a) >= 50000 && !(tune_flags() & 8)) {  // big-M stride-2 / two-segment: A from registers
-      rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
+      if (tune_flags() & 256)  // tap-major K order (A/B)
+        rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY & ~524288>(b, st);
+      else
+        rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
     }
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
     if (!ok(rc) && b.ksplit > 1) {  // K not divisible into the slices: no split

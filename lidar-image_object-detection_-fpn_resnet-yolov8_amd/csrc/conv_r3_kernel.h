@@ -299,6 +299,12 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
 // 16384 = scalar tap decode + per-lane tap validity masks for the A addresses (one segment,
 // C >= 32, checked at launch),
 // 8192 = W fragments read 3 column blocks ahead (4-slot ring, NSTAGE 2) instead of 2,
+// 524288 = channel-chunk-major K order over segment 0 (a 3x3 window, C % 32 == 0): K-tile kt covers tap kt % 9 of
+// the 32-channel chunk kt / 9 (weight columns tap * C + 32 chunk .. +31), so the blocks resident
+// on one XCD sweep a 32-channel slice of their input window through all 9 taps before the next
+// slice: that slice (~1-2 MB per XCD for the heads) stays in the 4 MB L2, where the tap-major
+// order's whole-window working set (4-9 MB per XCD at C = 128 / 256) re-read the input from
+// the fabric at every tap (heads L0 / L1: 7x / 5x their input in HBM traffic),
 // 2048 = transposed accumulators (W fragment as the MFMA A operand) with the float4 / shuffle
 // epilogues above, 4096 = fp16 split in 2 VALU per value (split2h_x8, inline v_fma_mix),
 // 256 = spread the W DMA: A loads at block 0, then one W piece per block from block 2, the two
@@ -393,6 +399,21 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   // (scalar), and each lane keeps a validity bit per tap and sub-tile row and the byte offset of
   // its pixel + channel group, so an A address costs a bit test, an add and a select.
   constexpr bool FAST_A = (ABL & 16384) != 0 && NSEG == 1;  // two-segment launches are refused
+  // chunk-major K order over segment 0 (a 3x3 window, checked at launch); segment 1 (the fused
+  // 1x1 downsample) keeps its order after it
+  constexpr bool CMAJ = (ABL & 524288) != 0;
+  const int cmaj_tiles = NSEG == 2 ? a.kseg1 / BK : a.Kpad / BK;  // K-tiles of segment 0
+  // first weight column of K-tile kt: tap * C + chunk * 32 (chunk-major) or kt * BK
+  auto kcol = [&](int kt) -> int {
+    if constexpr (CMAJ) {
+      if (NSEG == 1 || kt < cmaj_tiles) {
+        const int chunk = (kt * 7282) >> 16;  // kt / 9 for kt < 3640 (checked at launch)
+        return (kt - 9 * chunk) * a.seg[0].C + chunk * BK;
+      }
+    }
+    return kt * BK;
+  };
+
   unsigned vmask[TM], abase[TM];
   if constexpr (FAST_A) {
     const ConvSeg& sg0 = a.seg[0];
@@ -443,7 +464,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
     }
   };
   auto load_a = [&](int kt) {
-    const int k0 = kt * BK;
+    const int k0 = kcol(kt);
     if constexpr (FAST_A) {
       load_a_fast(k0);
     } else if constexpr (NSEG == 2) {
@@ -459,10 +480,10 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
     if (NB_REM == 0 || j < NB - 1 || wave < NB_REM)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rsw, (__attribute__((address_space(3))) void*)(S + (wave + NW * j) * 1024), 16,
-          (unsigned)(wlane + boff_s[j] + 2 * kt * BK), 0, 0, 0);
+          (unsigned)(wlane + boff_s[j] + 2 * kcol(kt)), 0, 0, 0);
   };
   auto load_w = [&](int kt, unsigned char* S) {
-    const int k0 = kt * BK;
+    const int k0 = kcol(kt);
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
       if (NB_REM == 0 || j < NB - 1 || wave < NB_REM)
@@ -702,6 +723,13 @@ inline int launch_conv_r3_cfg(const ConvArgs& a, hipStream_t st) {
   }
   if ((ABL & 16384) != 0 && (a.nseg != 1 || a.seg[0].C < 32 || a.seg[0].taps > 32)) {
     set_error("conv_r3: fast A addressing needs one segment with C >= 32 (C=%d)", a.seg[0].C);
+    return SFA_E_UNSUPPORTED;
+  }
+  if ((ABL & 524288) != 0 && (a.seg[0].taps != 9 || a.seg[0].C % 32 != 0 ||
+                              (a.nseg == 2 ? a.kseg1 : a.Kpad) != 9 * a.seg[0].C || a.Kpad / 32 > 3600 ||
+                              a.wstride || a.wk0)) {
+    set_error("conv_r3: chunk-major K order needs a 3x3 first segment with C %% 32 == 0 (C=%d Kpad=%d)", a.seg[0].C,
+              a.Kpad);
     return SFA_E_UNSUPPORTED;
   }
   for (int s = 0; s < a.nseg; ++s)

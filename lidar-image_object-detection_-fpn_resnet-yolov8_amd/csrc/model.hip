@@ -295,6 +295,11 @@ struct sfa_model {
   hipEvent_t fork = nullptr, join = nullptr, mid = nullptr;
   int device = -1;
   std::mutex fork_mu;  // fork ... join of one forward is not interleaved with another's
+  // Kernel probe (sfa_model_set_probe): timing events around each head-level launch, recorded
+  // on the stream that launches it (never while that stream is being captured); PROBE_SERIAL
+  // keeps every launch on the caller's stream so each head launch has the chip to itself.
+  int probe = 0;
+  hipEvent_t probe_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 
 extern "C" int sfa_abi_version(void) { return SFA_ABI_VERSION; }
@@ -454,6 +459,8 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
 
 extern "C" void sfa_model_destroy(sfa_model* model) {
   if (!model) return;
+  for (hipEvent_t e : model->probe_ev)
+    if (e) (void)hipEventDestroy(e);
   if (model->fork) (void)hipEventDestroy(model->fork);
   if (model->join) (void)hipEventDestroy(model->join);
   if (model->mid) (void)hipEventDestroy(model->mid);
@@ -470,6 +477,26 @@ extern "C" int sfa_model_set_math(sfa_model* model, int math) {
 }
 
 extern "C" int sfa_model_get_math(const sfa_model* model) { return model ? model->math : -1; }
+
+extern "C" int sfa_model_set_probe(sfa_model* model, int flags) {
+  SFA_CHECK_ARG(model, "set_probe: null model");
+  SFA_CHECK_ARG((flags & ~(SFA_PROBE_HEADS | SFA_PROBE_SERIAL)) == 0, "set_probe: unknown flags %d", flags);
+  if (flags & SFA_PROBE_HEADS)
+    for (hipEvent_t& e : model->probe_ev)
+      if (!e) SFA_HIP_TRY(hipEventCreate(&e));
+  model->probe = flags;
+  return SFA_OK;
+}
+
+extern "C" int sfa_model_probe_times(const sfa_model* model, float* ms, int n) {
+  SFA_CHECK_ARG(model && ms && n >= 0 && n <= 3, "probe_times: bad arguments");
+  SFA_CHECK_ARG(model->probe & SFA_PROBE_HEADS, "probe_times: probe not enabled");
+  for (int f = 0; f < n; ++f) {
+    SFA_HIP_TRY(hipEventSynchronize(model->probe_ev[2 * f + 1]));
+    SFA_HIP_TRY(hipEventElapsedTime(&ms[f], model->probe_ev[2 * f], model->probe_ev[2 * f + 1]));
+  }
+  return SFA_OK;
+}
 
 namespace sfa {
 
@@ -768,7 +795,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   const float* lin[3] = {F(bf.up2), F(bf.up3), F(bf.up4)};
   const int lh[3] = {H8, H4, H4}, lw[3] = {W8, W4, W4};
   float* lout[3] = {F(bf.L0), F(bf.L1), F(bf.L2)};
-  auto launch_head = [&](int f, hipStream_t hs) {
+  auto launch_head = [&](int f, hipStream_t hs) -> int {
     const PHeads& hp = p.heads[f];
     ConvArgs a;
     memset(&a, 0, sizeof a);
@@ -793,12 +820,19 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       a.hoff[j] = hoff[j];
     }
     a.hout = lout[f];
-    return launch_conv(a, EPI_HEAD, m->math, hs);
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    const bool probe = (m->probe & SFA_PROBE_HEADS) && hipStreamIsCapturing(hs, &cap) == hipSuccess &&
+                       cap == hipStreamCaptureStatusNone;
+    if (probe) SFA_HIP_TRY(hipEventRecord(m->probe_ev[2 * f], hs));
+    SFA_RC(launch_conv(a, EPI_HEAD, m->math, hs));
+    if (probe) SFA_HIP_TRY(hipEventRecord(m->probe_ev[2 * f + 1], hs));
+    return SFA_OK;
   };
   // level 0 needs only up_level2: fork it onto the side stream (graph capture follows
   // the event edges), join before apply_kfpn
   int sdev = -1;
-  const bool overlap = m->side && hipStreamGetDevice(st, &sdev) == hipSuccess && sdev == m->device;
+  const bool overlap = m->side && !(m->probe & SFA_PROBE_SERIAL) && hipStreamGetDevice(st, &sdev) == hipSuccess &&
+                       sdev == m->device;
   std::unique_lock<std::mutex> fork_lock(const_cast<sfa_model*>(m)->fork_mu, std::defer_lock);
   if (overlap) {
     fork_lock.lock();

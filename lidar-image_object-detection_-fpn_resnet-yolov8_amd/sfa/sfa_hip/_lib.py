@@ -75,6 +75,9 @@ _PROTOS = {
 MATH_F32, MATH_BF16X6, MATH_FP16X3 = 0, 1, 2
 _PROTOS["sfa_model_set_math"] = (_c_int, [_vp, _c_int])
 _PROTOS["sfa_model_get_math"] = (_c_int, [_vp])
+PROBE_HEADS, PROBE_SERIAL = 1, 2
+_PROTOS["sfa_model_set_probe"] = (_c_int, [_vp, _c_int])
+_PROTOS["sfa_model_probe_times"] = (_c_int, [_vp, ctypes.POINTER(ctypes.c_float), _c_int])
 
 
 def math_from_env(default=MATH_FP16X3) -> int:

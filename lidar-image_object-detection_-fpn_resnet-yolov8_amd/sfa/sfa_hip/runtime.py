@@ -83,6 +83,18 @@ class KfpnEngine:
         check(lib().sfa_model_set_math(self._h, int(math)), "sfa_model_set_math")
         self.math = int(math)
 
+    def set_probe(self, flags: int):
+        """Kernel probe (measurement only): _lib.PROBE_HEADS records timing events around each
+        head-level launch of un-captured forwards; _lib.PROBE_SERIAL keeps every launch on the
+        caller's stream. 0 turns it off."""
+        check(lib().sfa_model_set_probe(self._h, int(flags)), "sfa_model_set_probe")
+
+    def probe_times(self, levels: int = 3):
+        """Durations (ms) of the head-level launches of the last probed forward (waits for them)."""
+        ms = (ctypes.c_float * levels)()
+        check(lib().sfa_model_probe_times(self._h, ms, levels), "sfa_model_probe_times")
+        return [float(v) for v in ms]
+
     def __del__(self):
         try:
             if getattr(self, "_h", None) is not None and self._h.value:

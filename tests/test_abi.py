@@ -176,6 +176,20 @@ def test_argument_errors_before_any_launch():
     assert L.sfa_bev_voxelize(p, offs, 0, bnd, 0, 2, p, p, None) == -1
     assert L.sfa_bev_voxelize(p, offs, 1, bnd, 7, 2, p, p, None) == -1
     assert L.sfa_bev_scratch_size(16) == 16 * 608 * 608 * 12
+    # kernel probe (bench roofline): null model / unknown flags / reading a disabled probe
+    ms = (ctypes.c_float * 3)()
+    assert L.sfa_model_set_probe(None, _lib.PROBE_SERIAL) == -1
+    assert L.sfa_model_probe_times(None, ms, 3) == -1
+    arch = _lib.make_arch(gc.HEADS)
+    h = ctypes.c_void_p()
+    assert L.sfa_model_create(ctypes.byref(arch), p, ctypes.byref(h)) == 0
+    try:
+        assert L.sfa_model_set_probe(h, 8) == -1 and b"flags" in L.sfa_last_error_string()
+        assert L.sfa_model_set_probe(h, _lib.PROBE_SERIAL) == 0  # no events needed
+        assert L.sfa_model_probe_times(h, ms, 3) == -1 and b"not enabled" in L.sfa_last_error_string()
+        assert L.sfa_model_probe_times(h, ms, 4) == -1
+    finally:
+        L.sfa_model_destroy(h)
 
 
 def test_workspace_sizes():

@@ -265,8 +265,8 @@ int main(int argc, char** argv) {
       CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDTA(128, 128, 32, EPI_STD, 2, 2058),
   };
   std::vector<Cand> heads = {
-      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 96516, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 88324, 1),
-      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 88324, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 3, 88068, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 96516, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 620804, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 96516, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 620804, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
