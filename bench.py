@@ -190,6 +190,20 @@ def traffic_per_forward(args):
         return int(json.load(f)["conv_hbm_bytes_per_forward"])
 
 
+def head_traffic_per_launch(args):
+    """HBM bytes per head launch (mean over the 3 levels) from the committed PMC pass
+    (tools/pmc_forward.sh: FETCH_SIZE x2 + WRITE_SIZE per dispatch, the probe's serial forward)."""
+    if args.workload != "bev_infer" or args.batch != 16 or args.math != "fp16x3":
+        return None
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_forward_{args.math}.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        rows = [r for r in json.load(f)["per_launch"] if r["kernel"].startswith("sfa::conv_r3_kernel<256, 320")]
+    return int(sum(r["hbm_MB"] for r in rows) * 1e6 / len(rows)) if len(rows) == 3 else None
+
+
 def head_flop_per_launch(args):
     """Algorithmic f32 FLOP of one head-level launch: the 5 heads' 3x3 convs
     (C_l -> 64 each, as one N = 320 GEMM) + their 1x1 convs (64 -> c_h), over B frames."""
@@ -250,7 +264,9 @@ def roofline_line(args, heads, forward_roofline, fwd_achieved, peak, peak_basis,
         "launch_us": [round(1e3 * v, 1) for v in heads],
         "avg_launch_us": round(1e3 * sum(heads) / 3, 1),
         "algorithmic_flop_per_launch": flops,
-        "traffic": None,
+        "traffic": head_traffic_per_launch(args),
+        "traffic_basis": "HBM bytes per launch, mean of the 3 levels: PMC 2 x FETCH_SIZE + WRITE_SIZE "
+                         "(tools/pmc_forward.sh, profiles/r*_pmc_forward_%s.json)" % args.math,
     })
     return line
 

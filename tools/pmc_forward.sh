@@ -9,6 +9,6 @@ i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $grp --output-format csv -d "$OUT/p$i" -o run -- \
-    python bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline > "$OUT/p$i.log" 2>&1 \
+    python bench.py --steps 2 --warmup 1 --no-graph --no-cpu-baseline --probe-forwards 1 > "$OUT/p$i.log" 2>&1 \
     || { echo "pass $i failed: $grp" >> "$OUT/failed.txt"; exit 1; }
 done
