@@ -256,17 +256,21 @@ int main(int argc, char** argv) {
   };
   // round 2: conv_r3_kernel (A in registers) against the round-1 defaults (first entry of each)
   std::vector<Cand> n64 = {
-      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDTA(128, 64, 32, EPI_STD, 3, 2190),
+      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDR(256, 64, 32, EPI_STD, 2, 2, 554752, 1),
+      CANDR(128, 64, 32, EPI_STD, 4, 2, 554752, 1), CANDR(256, 64, 64, EPI_STD, 2, 2, 554752, 1),
+      CANDR(128, 64, 32, EPI_STD, 4, 2, 546560, 1),
   };
   std::vector<Cand> stem = {
       CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
   };
   std::vector<Cand> nbig = {
-      CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDTA(128, 128, 32, EPI_STD, 2, 2058),
+      CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDR(128, 128, 32, EPI_STD, 2, 2, 554752, 1),
+      CANDR(128, 128, 32, EPI_STD, 2, 2, 546560, 1), CANDR(256, 128, 32, EPI_STD, 1, 2, 554752, 1),
   };
   std::vector<Cand> heads = {
-      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 96516, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 620804, 1),
-      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 96516, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 620804, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 2, 620804, 1), CANDR(128, 320, 32, EPI_HEAD, 2, 2, 620804, 1),
+      CANDR(192, 320, 32, EPI_HEAD, 1, 2, 620804, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 620804, 1),
+      CANDR(128, 320, 32, EPI_HEAD, 2, 2, 620804, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
