@@ -286,7 +286,7 @@ def test_round2_kernels_match_round1(golden, gpu, monkeypatch, hw):
         assert e <= 1e-4, h
 
 
-@pytest.mark.parametrize("tune", ["0", "28", "32"])
+@pytest.mark.parametrize("tune", ["0", "28", "32", "256"])
 def test_batch_invariance_608(golden, gpu, monkeypatch, tune):
     """At the full 608x608 size (every kernel path of the bench: r3 heads, strip convs, FPN skip
     convs, r3 body convs (M >= 50000 needs >= 9 frames), split-K layer4): frames 7, 8 of a batch
@@ -303,3 +303,26 @@ def test_batch_invariance_608(golden, gpu, monkeypatch, tune):
     for h in gc.HEADS:
         np.testing.assert_array_equal(full[h], again[h], err_msg=f"{h}: repeated forward differs")
         np.testing.assert_array_equal(full[h][7:9], two[h], err_msg=f"{h}: batch of 10 vs batch of 2")
+
+
+def test_head_probe_is_transparent(golden, gpu):
+    """The bench's kernel probe (sfa_model_set_probe: timing events around the head launches, all
+    launches on the caller's stream) changes no result bit and times every head level."""
+    from sfa_hip import _lib
+    model = make_model(golden, gpu)
+    eng = model._engine(gpu)
+    eng.set_math(_math("fp16x3"))
+    x = torch.from_numpy(synthetic.synthetic_bev(3, 160, 192, seed=37)).to(gpu)
+    with torch.no_grad():
+        base = {h: v.cpu().numpy() for h, v in model(x).items()}
+        eng.set_probe(_lib.PROBE_HEADS | _lib.PROBE_SERIAL)
+        try:
+            probed = {h: v.cpu().numpy() for h, v in model(x).items()}
+            ms = eng.probe_times(3)
+        finally:
+            eng.set_probe(0)
+        after = {h: v.cpu().numpy() for h, v in model(x).items()}
+    assert len(ms) == 3 and all(t > 0 for t in ms), ms
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(base[h], probed[h], err_msg=f"{h}: probed forward differs")
+        np.testing.assert_array_equal(base[h], after[h], err_msg=f"{h}: forward after the probe differs")
