@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--inflight", type=int, default=2,
                     help="steps in flight on separate streams (each with its own buffers and "
                          "model handle); >1 lets one step's kernel tails overlap the next's")
+    ap.add_argument("--stream-inflight", type=int, default=1,
+                    help="--workload stream: pipelines in flight (profiles/r02_stream_variants.txt)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--serial-heads", action="store_true",
                     help="keep the level-0 heads on the main stream (no side stream) for the whole "
@@ -320,12 +322,12 @@ def run_stream(args, rank, world, dev):
             files.append(p)
         threads = max(1, min(16, len(os.sched_getaffinity(0)) // max(1, world)))
         warm = StreamingDetector(engine, [files[i % len(files)] for i in range(args.batch * args.warmup)],
-                                 args.batch, args.K, threads)
+                                 args.batch, args.K, threads, inflight=args.stream_inflight, graph=not args.no_graph)
         warm.run()
         torch.cuda.synchronize()
         warm.close()
         det = StreamingDetector(engine, [files[i % len(files)] for i in range(args.batch * args.steps)],
-                                args.batch, args.K, threads)
+                                args.batch, args.K, threads, inflight=args.stream_inflight, graph=not args.no_graph)
         if world > 1:
             import torch.distributed as dist
             dist.barrier()
@@ -408,8 +410,8 @@ def main():
             if args.workload == "stream":
                 data = "synthetic 132,880-pt sweeps written as KITTI .bin files (page cache)"
                 cfg = {"workload": "KITTI .bin stream -> pinned DMA -> BEV -> fpn_resnet_18 "
-                                   "forward -> decode K=%d, bs=%d per GPU (no HIP graph: "
-                                   "per-batch frame offsets)" % (args.K, args.batch),
+                                   "forward -> decode K=%d, bs=%d per GPU (forward + decode as a "
+                                   "HIP graph, BEV eager: per-batch frame offsets)" % (args.K, args.batch),
                        "reader_threads": threads, "global_batch": world * args.batch}
             else:
                 data = ("synthetic 132,880-pt sweeps + 30 synthetic camera boxes per frame "

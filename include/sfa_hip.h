@@ -113,12 +113,13 @@ size_t sfa_packed_floats(const sfa_arch* arch);
 int sfa_pack_weights(const sfa_arch* arch, const float* state, size_t state_floats, float* packed);
 
 /* A model handle references a device copy of the packed weights (caller-owned,
- * must outlive the handle).  No device memory is allocated.  The handle owns one side
- * stream + two events on the device current at creation: a forward on a stream of that
- * device runs the level-0 detection heads on the side stream, overlapping the rest of the
- * FPN and the level-1/2 heads (forked/joined by events, so HIP-graph capture of the
- * caller's stream records both branches); on another device everything stays on the
- * caller's stream. */
+ * must outlive the handle).  No device memory is allocated.  The handle owns side
+ * streams + events on the device current at creation: a forward on a stream of that
+ * device runs the level-0 detection heads on a side stream (overlapping the rest of the FPN)
+ * and the level-2 heads beside the level-1 heads (env SFA_FPN3_SIDE=1: the last FPN conv
+ * pair too, on a second side stream), forked/joined by events, so HIP-graph capture of the
+ * caller's stream records every branch; on another device everything stays on the caller's
+ * stream. */
 typedef struct sfa_model sfa_model;
 int sfa_model_create(const sfa_arch* arch, const float* packed_device, sfa_model** out);
 void sfa_model_destroy(sfa_model* model);
@@ -142,7 +143,7 @@ int sfa_model_get_math(const sfa_model* model);
  * forward NOT being captured into a graph records a timing event before and after each
  * detection-head level's launch (the dominant kernel, 54.6 % of the FLOPs), on the stream
  * that launches it; SFA_PROBE_SERIAL: all launches stay on the caller's stream (no
- * level-0 side stream), so each head launch has the chip to itself.  sfa_model_probe_times
+ * side streams), so each head launch has the chip to itself.  sfa_model_probe_times
  * waits for the last probed forward's events and returns the launch durations of head
  * levels 0 .. n-1 in ms.  flags = 0 turns the probe off. */
 enum sfa_probe_flags { SFA_PROBE_HEADS = 1, SFA_PROBE_SERIAL = 2 };

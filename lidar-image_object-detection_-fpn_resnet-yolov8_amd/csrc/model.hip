@@ -293,6 +293,13 @@ struct sfa_model {
   // used only when the forward's stream is on that device.
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr, mid = nullptr;
+  // Second side stream (env SFA_FPN3_SIDE=1): the last FPN conv pair (conv_up_level3, ->
+  // up_level4) and the level-2 heads there, beside the level-1 heads, which need only
+  // up_level3. Off by default: the single-step forward gains 1-2 %, but with two steps in
+  // flight (the bench) the extra concurrency costs 1.7 % (profiles/r02_ab_fpn3_side.txt).
+  hipStream_t side2 = nullptr;
+  hipEvent_t join2 = nullptr;
+  bool fpn3_side = false;  // (created only when enabled: every stream takes a hardware queue)
   int device = -1;
   std::mutex fork_mu;  // fork ... join of one forward is not interleaved with another's
   // Kernel probe (sfa_model_set_probe): timing events around each head-level launch, recorded
@@ -444,11 +451,16 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   if (const char* e = getenv("SFA_STEM_PATCH")) m->stem_patch = strcmp(e, "0") != 0;
   if (const char* e = getenv("SFA_STEM_PATCH_ATOMIC")) m->stem_atomic = strcmp(e, "0") != 0;
   if (const char* e = getenv("SFA_FPN_COMMUTE")) m->fpn_commute = atoi(e) & 7;
-  if (hipGetDevice(&m->device) != hipSuccess ||
+  if (const char* e = getenv("SFA_FPN3_SIDE")) m->fpn3_side = strcmp(e, "0") != 0;
+  bool side_streams = true;  // env SFA_SIDE_STREAMS=0: every launch on the caller's stream (A/B)
+  if (const char* e = getenv("SFA_SIDE_STREAMS")) side_streams = strcmp(e, "0") != 0;
+  if (!side_streams || hipGetDevice(&m->device) != hipSuccess ||
       hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&m->fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&m->join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&m->mid, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&m->mid, hipEventDisableTiming) != hipSuccess ||
+      (m->fpn3_side && (hipStreamCreateWithFlags(&m->side2, hipStreamNonBlocking) != hipSuccess ||
+                        hipEventCreateWithFlags(&m->join2, hipEventDisableTiming) != hipSuccess))) {
     // no device (or no stream): the forward runs every launch on the caller's stream
     (void)hipGetLastError();
     m->side = nullptr;
@@ -464,6 +476,8 @@ extern "C" void sfa_model_destroy(sfa_model* model) {
   if (model->fork) (void)hipEventDestroy(model->fork);
   if (model->join) (void)hipEventDestroy(model->join);
   if (model->mid) (void)hipEventDestroy(model->mid);
+  if (model->join2) (void)hipEventDestroy(model->join2);
+  if (model->side2) (void)hipStreamDestroy(model->side2);
   if (model->side) (void)hipStreamDestroy(model->side);
   delete model;
 }
@@ -745,7 +759,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   float* fpn_lo[3] = {F(bf.up1), F(bf.up1) + (size_t)B * (H / 32) * (W / 32) * 256,
                       F(bf.up1) + (size_t)B * (H / 32) * (W / 32) * 256 + (size_t)B * H16 * W16 * 128};
   auto fpn_pair = [&](int f, const float* x, int xh, int xw, int xc, int xslot_in, const float* skip, int sc,
-                      int skip_slot, float* out, int out_slot) -> int {
+                      int skip_slot, float* out, int out_slot, hipStream_t fs) -> int {
     const PConv& pc = p.fpn[f];
     {
       ConvArgs a = conv_args(wb, pc, B, xh, xw, fpn_lo[f], nullptr, 0);
@@ -755,7 +769,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       a.wk0 = 0;
       a.seg[0] = seg(x, B, xh, xw, xc, 1, 1, 0);
       io(a, xslot_in, -1, -1);
-      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+      SFA_RC(launch_conv(a, EPI_STD, m->math, fs));
     }
     ConvArgs a = conv_args(wb, pc, B, 2 * xh, 2 * xw, out, nullptr, 0);
     a.Kpad = sc;
@@ -766,11 +780,11 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.res_sh = xh > 1 ? (float)(xh - 1) / (float)(2 * xh - 1) : 0.f;
     a.res_sw = xw > 1 ? (float)(xw - 1) / (float)(2 * xw - 1) : 0.f;
     io(a, skip_slot, -1, out_slot);
-    return launch_conv(a, EPI_STD, m->math, st);
+    return launch_conv(a, EPI_STD, m->math, fs);
   };
   if (commute_at(0)) {
     SFA_RC(fpn_pair(0, F(bf.l[3]), H / 32, W / 32, 512, blk_slot(3, 1, 1), F(bf.l[2]), 256, blk_slot(2, 1, 1),
-                    F(bf.c1), AM_FPN + 0));
+                    F(bf.c1), AM_FPN + 0, st));
   } else {
     SFA_RC(launch_upsample2x(F(bf.l[3]), F(bf.up1), B, H / 32, W / 32, 512, st));
     {
@@ -833,6 +847,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   int sdev = -1;
   const bool overlap = m->side && !(m->probe & SFA_PROBE_SERIAL) && hipStreamGetDevice(st, &sdev) == hipSuccess &&
                        sdev == m->device;
+  const bool side2_on = overlap && m->side2 && m->fpn3_side;
   std::unique_lock<std::mutex> fork_lock(const_cast<sfa_model*>(m)->fork_mu, std::defer_lock);
   if (overlap) {
     fork_lock.lock();
@@ -842,6 +857,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   // Everything between the fork and the join: any failure inside returns from this lambda
   // only, so the side stream is still joined below (a graph capture stays valid, no work is
   // left orphaned on the side stream).
+  bool side2_forked = false;  // side2 joined this forward (graph capture: it must be joined back)
   auto forked = [&]() -> int {
   if (overlap) {
     SFA_RC(launch_head(0, m->side));
@@ -850,7 +866,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   }
   if (commute_at(1)) {
     SFA_RC(fpn_pair(1, F(bf.c1), H16, W16, 256, AM_FPN + 0, F(bf.l[1]), 128, blk_slot(1, 1, 1), F(bf.c2),
-                    AM_FPN + 1));
+                    AM_FPN + 1, st));
   } else
   {
     ConvArgs a = conv_args(wb, p.fpn[1], B, H8, W8, F(bf.c2), nullptr, 0);
@@ -862,19 +878,31 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     SFA_RC(launch_conv(a, EPI_STD, m->math, st));
   }
   SFA_RC(launch_upsample2x(F(bf.c2), F(bf.up3), B, H8, W8, 128, st));
-  if (commute_at(2)) {
-    SFA_RC(fpn_pair(2, F(bf.c2), H8, W8, 128, AM_FPN + 1, F(bf.l[0]), 64, blk_slot(0, 1, 1), F(bf.up4),
-                    AM_FPN + 2));
-  } else
-  {
+  // FPN level 3 (-> up_level4) on stream fs
+  auto fpn3 = [&](hipStream_t fs) -> int {
+    if (commute_at(2))
+      return fpn_pair(2, F(bf.c2), H8, W8, 128, AM_FPN + 1, F(bf.l[0]), 64, blk_slot(0, 1, 1), F(bf.up4),
+                      AM_FPN + 2, fs);
     ConvArgs a = conv_args(wb, p.fpn[2], B, H4, W4, F(bf.up4), nullptr, 0);
     a.nseg = 2;
     a.kseg1 = 128;
     a.seg[0] = seg(F(bf.up3), B, H4, W4, 128, 1, 1, 0);
     a.seg[1] = seg(F(bf.l[0]), B, H4, W4, 64, 1, 1, 0);
     io(a, AM_FPN + 1, blk_slot(0, 1, 1), AM_FPN + 2);
-    SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+    return launch_conv(a, EPI_STD, m->math, fs);
+  };
+  if (side2_on) {
+    // up_level3 is written: FPN level 3 + the level-2 heads on side2, the level-1 heads here,
+    // side by side (neither waits for the other)
+    SFA_HIP_TRY(hipEventRecord(m->mid, st));
+    SFA_HIP_TRY(hipStreamWaitEvent(m->side2, m->mid, 0));
+    side2_forked = true;
+    SFA_RC(fpn3(m->side2));
+    SFA_RC(launch_head(2, m->side2));
+    SFA_RC(launch_head(1, st));
+    return SFA_OK;
   }
+  SFA_RC(fpn3(st));
   // level 2 (needs up_level4, just written) on the side stream after level 0, level 1 here:
   // the two 1,444-tile launches run side by side, so neither one's last partial wave of tiles
   // leaves CUs idle
@@ -891,6 +919,10 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   if (overlap) {  // the join, on success and on failure alike
     SFA_HIP_TRY(hipEventRecord(m->join, m->side));
     SFA_HIP_TRY(hipStreamWaitEvent(st, m->join, 0));
+    if (side2_forked) {
+      SFA_HIP_TRY(hipEventRecord(m->join2, m->side2));
+      SFA_HIP_TRY(hipStreamWaitEvent(st, m->join2, 0));
+    }
   }
   SFA_RC(frc);
   // apply_kfpn (fpn_resnet.py:248-254)

@@ -83,6 +83,21 @@ class KfpnEngine:
         check(lib().sfa_model_set_math(self._h, int(math)), "sfa_model_set_math")
         self.math = int(math)
 
+    def twin(self) -> "KfpnEngine":
+        """A second model handle over the SAME device weights (sfa_model_create does not copy
+        them): its own side stream and events, so two forwards can be in flight (or captured in
+        two graphs) on two streams. Workspaces are per engine / pipeline as usual."""
+        t = object.__new__(KfpnEngine)
+        t.arch, t.device, t.heads, t.weights = self.arch, self.device, self.heads, self.weights
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(lib().sfa_model_create(ctypes.byref(self.arch), self.weights.data_ptr(), ctypes.byref(h)),
+                  "sfa_model_create")
+        t._h = h
+        t._ws = {}
+        t.set_math(self.math)
+        return t
+
     def set_probe(self, flags: int):
         """Kernel probe (measurement only): _lib.PROBE_HEADS records timing events around each
         head-level launch of un-captured forwards; _lib.PROBE_SERIAL keeps every launch on the
@@ -357,6 +372,7 @@ class DetectorPipeline:
             else:
                 self.x = torch.empty((batch, 3, height, width), dtype=torch.float32, device=self.dev)
         self.graph = None
+        self.infer_graph = None  # forward + decode only (capture_infer): the BEV stays eager
 
     def set_points(self, clouds):
         """Copy a list of (N_i, 4) float32 clouds into the resident point buffer."""
@@ -391,6 +407,13 @@ class DetectorPipeline:
                          out=self.bev[self.B:], stream=st)
             if bev_done is not None:
                 bev_done.record(torch.cuda.current_stream(self.dev))
+        if self.infer_graph is not None:
+            self.infer_graph.replay()
+            return self.dets
+        return self._infer(st)
+
+    def _infer(self, st):
+        if self.with_bev:
             self.engine.forward_into(self.bev, self.outs, _lib.IN_NHWC4, self.ws, st)
         else:
             self.engine.forward_into(self.x, self.outs, _lib.IN_NCHW3, self.ws, st)
@@ -411,6 +434,22 @@ class DetectorPipeline:
             with torch.cuda.graph(g):
                 self.run()
             self.graph = g
+        return g
+
+    def capture_infer(self):
+        """Capture the forward + decode (everything after the BEV) into a HIP graph that run()
+        replays: the voxeliser's launches depend on the batch's host frame offsets (a new
+        ragged batch per step when streaming), the rest of the step does not."""
+        with torch.cuda.device(self.dev):
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._infer(_lib.stream_ptr(self.dev))  # warm outside capture
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._infer(_lib.stream_ptr(self.dev))
+            self.infer_graph = g
         return g
 
     def replay(self):
@@ -645,6 +684,7 @@ class FusionPipeline:
             self.fkeep_count = torch.empty(batch, dtype=i32, device=dev)
         self.max_camera_boxes = max_camera_boxes
         self.graph = None
+        self.infer_graph = None  # forward + decode only (capture_infer): the BEV stays eager
 
     def set_points(self, clouds):
         self.det.set_points(clouds)
@@ -702,6 +742,22 @@ class FusionPipeline:
             with torch.cuda.graph(g):
                 self.run()
             self.graph = g
+        return g
+
+    def capture_infer(self):
+        """Capture the forward + decode (everything after the BEV) into a HIP graph that run()
+        replays: the voxeliser's launches depend on the batch's host frame offsets (a new
+        ragged batch per step when streaming), the rest of the step does not."""
+        with torch.cuda.device(self.dev):
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._infer(_lib.stream_ptr(self.dev))  # warm outside capture
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._infer(_lib.stream_ptr(self.dev))
+            self.infer_graph = g
         return g
 
     def replay(self):

@@ -90,40 +90,64 @@ class StreamingDetector:
     """.bin files -> (pinned DMA) -> BEV -> KFPN forward -> decode, one batch at a time, with
     the host reads and the H2D copy of batch k+1 overlapping the GPU work of batch k.
 
+    ``inflight`` pipelines (each with its own buffers and model handle, ``KfpnEngine.twin``)
+    take the batches in turn on their own streams; the forward + decode of each is a HIP graph
+    (``graph=True``), the voxeliser (ragged per-batch frame offsets) is launched eagerly.
+    Default 1: with the copy stream beside them, two pipelines' streams (and their side
+    streams) exceed the 4 hardware queues per process and measured 7 % slower
+    (profiles/r02_stream_variants.txt).
+
     ``run(callback)`` calls ``callback(dets_view, n_frames, batch_index)`` after each batch
-    is enqueued (dets are valid once the current stream reaches that point)."""
+    is enqueued, with that batch's stream current (dets are valid once that stream reaches
+    that point; work the callback enqueues there is ordered before the pipeline's reuse)."""
 
     def __init__(self, engine, paths, batch: int = 16, K: int = 50, n_threads: int = 8,
-                 max_points_per_frame: int = 200_000):
+                 max_points_per_frame: int = 200_000, inflight: int = 1, graph: bool = True):
         from .runtime import DetectorPipeline
         self.dev = engine.device
         self.batch = batch
-        self.pipe = DetectorPipeline(engine, batch, K=K, with_bev=True, max_points=1)
+        engines = [engine] + [engine.twin() for _ in range(max(1, int(inflight)) - 1)]
+        self.pipes = [DetectorPipeline(e, batch, K=K, with_bev=True, max_points=1) for e in engines]
+        if graph:
+            for p in self.pipes:
+                p.capture_infer()
         self.src = BinStream(paths, batch, batch * max_points_per_frame, n_threads, self.dev,
                              n_buffers=2)
 
+    @property
+    def pipe(self):
+        return self.pipes[0]
+
     def run(self, callback=None):
         with torch.cuda.device(self.dev):
-            comp = torch.cuda.current_stream()
+            main = torch.cuda.current_stream()
+            comps = [main] + [torch.cuda.Stream() for _ in range(len(self.pipes) - 1)]
+            for c in comps[1:]:
+                c.wait_stream(main)
             copy = torch.cuda.Stream()
-            ev_copy = [torch.cuda.Event(), torch.cuda.Event()]
-            ev_bev = [torch.cuda.Event(), torch.cuda.Event()]
+            nb = len(self.src.bufs)
+            ev_copy = [torch.cuda.Event() for _ in range(nb)]
+            ev_bev = [torch.cuda.Event() for _ in range(nb)]
             item = self.src.next(copy.cuda_stream)
             ev_copy[0].record(copy)
             k = 0
             while item is not None:
                 pts, offs = item
-                comp.wait_event(ev_copy[k % 2])
-                self.pipe.load_points(pts, offs)
-                self.pipe.run(bev_done=ev_bev[k % 2])
-                if callback is not None:
-                    callback(self.pipe.dets, len(offs) - 1, k)
-                # the buffer of batch k-1 is free once its BEV pass is done
-                if k >= 1:
-                    copy.wait_event(ev_bev[(k + 1) % 2])
+                pipe, comp = self.pipes[k % len(self.pipes)], comps[k % len(comps)]
+                with torch.cuda.stream(comp):
+                    comp.wait_event(ev_copy[k % nb])
+                    pipe.load_points(pts, offs)
+                    pipe.run(bev_done=ev_bev[k % nb])
+                    if callback is not None:
+                        callback(pipe.dets, len(offs) - 1, k)
+                # buffer (k + 1) % nb is free once the BEV pass of batch k + 1 - nb is done
+                if k + 1 >= nb:
+                    copy.wait_event(ev_bev[(k + 1) % nb])
                 item = self.src.next(copy.cuda_stream)
-                ev_copy[(k + 1) % 2].record(copy)
+                ev_copy[(k + 1) % nb].record(copy)
                 k += 1
+            for c in comps[1:]:
+                main.wait_stream(c)
             return k
 
     def close(self):
