@@ -77,6 +77,10 @@ def parse():
     ap.add_argument("--math", choices=list(MATHS), default=env_math,
                     help="convolution arithmetic (include/sfa_hip.h sfa_math; default: SFA_MATH "
                          "or the library default)")
+    ap.add_argument("--input", choices=["uniform", "sweeps"], default="uniform",
+                    help="bev_infer frames: U[0,1) in every cell (dense, the default), or the BEV maps "
+                         "of synthetic 132,880-point sweeps (sparse like KITTI; made on the GPU before "
+                         "the timed region)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--inflight", type=int, default=2,
                     help="steps in flight on separate streams (each with its own buffers and "
@@ -127,7 +131,15 @@ def build_pipeline(dev, args, rank):
         pipe.set_points(clouds)
     else:
         pipe = DetectorPipeline(engine, args.batch, K=args.K)
-        pipe.x.copy_(torch.from_numpy(synthetic.synthetic_bev(args.batch, seed=1 + rank)))
+        if args.input == "sweeps":
+            from sfa_hip.runtime import BevVoxelizer
+            clouds = [synthetic.synthetic_point_cloud(1000 * rank + i + 1) for i in range(args.batch)]
+            offs = np.cumsum([0] + [c.shape[0] for c in clouds])
+            pts = torch.from_numpy(np.concatenate(clouds)).to(dev)
+            BevVoxelizer(dev, args.batch)(pts, offs, layout=_lib.BEV_NCHW3_F32, out=pipe.x)
+            torch.cuda.synchronize()
+        else:
+            pipe.x.copy_(torch.from_numpy(synthetic.synthetic_bev(args.batch, seed=1 + rank)))
     return pipe
 
 
@@ -529,7 +541,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": DTYPES[args.math],
-            "data": "synthetic (hash-RNG U[0,1) BEV frames; synthetic He-uniform weights, BN folded)"
+            "data": ("synthetic (hash-RNG U[0,1) BEV frames; synthetic He-uniform weights, BN folded)"
+                     if args.input == "uniform" else
+                     "synthetic (BEV maps of synthetic 132,880-pt sweeps, SURVEY §8(d); synthetic weights)")
                     if args.workload == "bev_infer" else
                     "synthetic (132,880-pt LiDAR sweeps per frame, SURVEY §8(d); synthetic weights)",
             "config": {
