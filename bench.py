@@ -85,6 +85,9 @@ def parse():
     ap.add_argument("--inflight", type=int, default=2,
                     help="steps in flight on separate streams (each with its own buffers and "
                          "model handle); >1 lets one step's kernel tails overlap the next's")
+    ap.add_argument("--fusion-nms", choices=["greedy", "gaussian"], default="greedy",
+                    help="--workload fusion: test6.py's greedy NMS or the README's Gaussian soft-NMS "
+                         "(README.md:250-261)")
     ap.add_argument("--stream-inflight", type=int, default=1,
                     help="--workload stream: pipelines in flight (profiles/r02_stream_variants.txt)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -370,7 +373,7 @@ def run_fusion(args, rank, world, dev):
     cal = project_cases.calibs()["avg"]
     calib = runtime_make_calib(cal)
     clouds = [synthetic.synthetic_point_cloud(1000 * rank + i + 1) for i in range(args.batch)]
-    fp = FusionPipeline(engine, args.batch, [calib], K=args.K,
+    fp = FusionPipeline(engine, args.batch, [calib], K=args.K, nms=args.fusion_nms,
                         max_points=sum(c.shape[0] for c in clouds), conf_source=_lib.CONF_SCORE)
     fp.set_points(clouds)
     cams = []
@@ -430,7 +433,8 @@ def main():
                         "(YOLOv8n itself not in the framework)")
                 cfg = {"workload": "BASELINE configs[4]: sweeps -> BEV -> fpn_resnet_18 forward -> "
                                    "decode K=%d -> post_process -> camera boxes -> Bayesian "
-                                   "fusion + NMS, bs=%d per GPU, one HIP graph" % (args.K, args.batch),
+                                   "fusion + %s NMS, bs=%d per GPU, one HIP graph"
+                                   % (args.K, args.fusion_nms, args.batch),
                        "global_batch": world * args.batch}
             print(json.dumps({
                 "metric": METRIC, "value": round(frames / elapsed, 2), "unit": "frames/s",

@@ -309,6 +309,16 @@ typedef struct sfa_fusion_params {
 int sfa_iou_matrix(const int32_t* boxes_a, int na, const int32_t* boxes_b, int nb, double* out,
                    void* stream);
 
+/* Gaussian soft-NMS: replaces README.md:250-261 gaussian_nms(detections, sigma=0.5) (the
+ * reference's only definition of it): for each frame b, the count[b] detections at
+ * boxes/conf[start[b] ..] (DEVICE int32 starts/counts [batch]; boxes int32 [x,y,w,h] as
+ * calculate_iou, test6.py:76-101) are visited in order and every later one decays in place,
+ * conf[j] *= exp(-iou(i, j)^2 / sigma) for i < j in increasing i; order, boxes and count are
+ * unchanged (no threshold).  f64; a count <= 0 leaves the frame untouched.  Chains after
+ * sfa_fuse_detections with starts = yolo_offsets[b] + sfa_offsets[b], counts = out_count. */
+int sfa_gaussian_nms(int batch, const int32_t* boxes, double* conf, const int32_t* starts,
+                     const int32_t* counts, double sigma, void* stream);
+
 int sfa_fuse_detections(int batch, const int32_t* yolo_boxes, const double* yolo_conf,
                         const int32_t* yolo_cls, const int32_t* yolo_offsets,
                         const int32_t* sfa_boxes, const double* sfa_conf,

@@ -229,6 +229,31 @@ __global__ void __launch_bounds__(64) fuse_kernel(
   if (lane == 0) okeep_count[b] = nk;
 }
 
+// Gaussian soft-NMS (reference README.md:250-261 gaussian_nms; the only definition the
+// reference has, see SURVEY.md's north-star note): for i in order, every later detection j
+// decays, conf_j *= exp(-iou(i, j)^2 / sigma) — no re-sorting, no threshold, boxes unchanged.
+// conf_j's factors are therefore applied in i = 0 .. j-1 order, which lane j reproduces exactly
+// (f64, no contraction); exp is the device's f64 exp (numpy's np.exp may differ in the last
+// bit, so the confidences are pinned to ~1e-15 relative, not bitwise). One wave per frame.
+__global__ void __launch_bounds__(256) gaussian_nms_kernel(int batch, const int4* __restrict__ boxes,
+                                                           double* __restrict__ conf,
+                                                           const int32_t* __restrict__ starts,
+                                                           const int32_t* __restrict__ counts,
+                                                           double sigma) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (b >= batch) return;
+  const int n = counts[b], s0 = starts[b];
+  for (int j = lane; j < n; j += 64) {
+    const int4 bj = boxes[s0 + j];
+    double c = conf[s0 + j];
+    for (int i = 0; i < j; ++i) {
+      const double iou = box_iou(boxes[s0 + i], bj);  // calculate_iou(det_i, det_j), symmetric
+      c = c * exp(-(iou * iou) / sigma);
+    }
+    conf[s0 + j] = c;
+  }
+}
+
 __global__ void __launch_bounds__(256) iou_matrix_kernel(const int4* __restrict__ a, int na,
                                                          const int4* __restrict__ b, int nb,
                                                          double* __restrict__ out) {
@@ -276,6 +301,18 @@ extern "C" int sfa_fuse_detections(int batch, const int32_t* yolo_boxes, const d
                      reinterpret_cast<const int4*>(sfa_boxes), sfa_conf, sfa_offsets, a,
                      reinterpret_cast<int4*>(out_boxes), out_conf, out_cls, out_src, out_origin,
                      out_match, out_count, out_keep, out_keep_count);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+extern "C" int sfa_gaussian_nms(int batch, const int32_t* boxes, double* conf, const int32_t* starts,
+                                const int32_t* counts, double sigma, void* stream) {
+  SFA_CHECK_ARG(batch >= 0 && (batch == 0 || (boxes && conf && starts && counts)), "gaussian_nms: bad arguments");
+  SFA_CHECK_ARG(sigma > 0.0, "gaussian_nms: sigma must be > 0 (got %g)", sigma);
+  if (batch == 0) return SFA_OK;
+  hipLaunchKernelGGL(gaussian_nms_kernel, dim3((unsigned)((batch + 3) / 4)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), batch, reinterpret_cast<const int4*>(boxes), conf,
+                     starts, counts, sigma);
   SFA_LAUNCH_CHECK();
   return SFA_OK;
 }

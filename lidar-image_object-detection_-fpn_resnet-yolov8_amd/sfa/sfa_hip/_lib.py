@@ -103,6 +103,7 @@ class SfaFusionParams(ctypes.Structure):
 FUSE_BAYES, FUSE_WEIGHTED = 0, 1
 SRC_YOLO, SRC_LIDAR, SRC_FUSED = 0, 1, 2
 _PROTOS["sfa_iou_matrix"] = (_c_int, [_vp, _c_int, _vp, _c_int, _vp, _vp])
+_PROTOS["sfa_gaussian_nms"] = (_c_int, [_c_int, _vp, _vp, _vp, _vp, ctypes.c_double, _vp])
 _PROTOS["sfa_fuse_detections"] = (_c_int, [_c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                            ctypes.POINTER(SfaFusionParams), _vp, _vp, _vp, _vp,
                                            _vp, _vp, _vp, _vp, _vp, _vp])

@@ -473,6 +473,42 @@ def iou_matrix(boxes_a, boxes_b, device=None) -> torch.Tensor:
     return out
 
 
+def gaussian_nms_(boxes: torch.Tensor, conf: torch.Tensor, starts: torch.Tensor, counts: torch.Tensor,
+                  sigma: float = 0.5, stream: int = None) -> torch.Tensor:
+    """Gaussian soft-NMS in place on device arrays (README.md:250-261 gaussian_nms, batched):
+    boxes int32 (N, 4) [x, y, w, h], conf f64 (N,), frame b = the counts[b] entries from
+    starts[b] (int32 device tensors). Returns conf."""
+    for t, name, dt in ((boxes, "boxes", torch.int32), (conf, "conf", torch.float64),
+                        (starts, "starts", torch.int32), (counts, "counts", torch.int32)):
+        _require_gpu_tensor(t, "gaussian_nms " + name, dt)
+        if not t.is_contiguous():
+            raise ValueError(f"gaussian_nms: {name} must be contiguous (updated in place)")
+    if starts.numel() != counts.numel():
+        raise ValueError("gaussian_nms: starts and counts differ in length")
+    st = stream if stream is not None else _lib.stream_ptr(conf.device)
+    check(lib().sfa_gaussian_nms(int(starts.numel()), boxes.data_ptr() if boxes.numel() else None,
+                                 conf.data_ptr() if conf.numel() else None, starts.data_ptr(),
+                                 counts.data_ptr(), float(sigma), st), "sfa_gaussian_nms")
+    return conf
+
+
+def gaussian_nms_frames(frames, sigma: float = 0.5, device=None):
+    """[(boxes (n, 4) int, conf (n,) f64), ...] -> the decayed confidences per frame (host f64),
+    all frames in one launch."""
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    counts = np.array([len(c) for _, c in frames], np.int32)
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int32) if len(frames) else np.zeros(0, np.int32)
+    boxes = np.concatenate([np.asarray(b, np.int32).reshape(-1, 4) for b, _ in frames]) if len(frames) \
+        else np.zeros((0, 4), np.int32)
+    conf = np.concatenate([np.asarray(c, np.float64).reshape(-1) for _, c in frames]) if len(frames) \
+        else np.zeros(0, np.float64)
+    tb = torch.from_numpy(np.ascontiguousarray(boxes)).to(dev)
+    tc = torch.from_numpy(np.ascontiguousarray(conf)).to(dev)
+    gaussian_nms_(tb, tc, torch.from_numpy(starts).to(dev), torch.from_numpy(counts).to(dev), sigma)
+    out = tc.cpu().numpy()
+    return [out[s:s + n] for s, n in zip(starts, counts)]
+
+
 class FusionResult:
     """Per-frame fused lists (reference order) and NMS survivors (host arrays)."""
 
@@ -643,19 +679,27 @@ class FusionPipeline:
     device-resident CSR buffers, so run() is one HIP-graph-capturable sequence.
 
     The camera branch (YOLOv8n, ultralytics) is not part of this framework: its per-frame
-    boxes are inputs (``set_camera``), as test6.py:189-209 hands them to the fusion."""
+    boxes are inputs (``set_camera``), as test6.py:189-209 hands them to the fusion.
+
+    ``nms="gaussian"``: the fused lists get the README's Gaussian soft-NMS (README.md:250-261,
+    sfa_gaussian_nms: confidences decayed in place, ``fconf``) instead of the greedy NMS of
+    test6.py:104-126 (``fkeep`` then stays unused)."""
 
     def __init__(self, engine: KfpnEngine, batch: int, calibs, K: int = 50, max_points: int = 0,
                  max_camera_boxes: int = 512, conf_threshold=0.3, fusion_iou_threshold=0.7,
-                 nms_threshold=0.5, mode=_lib.FUSE_BAYES, conf_source=_lib.CONF_CLASS_ID):
+                 nms_threshold=0.5, mode=_lib.FUSE_BAYES, conf_source=_lib.CONF_CLASS_ID,
+                 nms: str = "greedy", soft_nms_sigma: float = 0.5):
         self.det = DetectorPipeline(engine, batch, K=K, with_bev=True, max_points=max_points)
         self.B, self.K, self.dev = batch, K, engine.device
         dev = self.dev
         calibs = list(calibs)
         self.calib = calib_tensor(calibs, dev)
         self.conf_source = conf_source
+        if nms not in ("greedy", "gaussian"):
+            raise ValueError(f"nms must be 'greedy' or 'gaussian', got {nms!r}")
+        self.nms, self.soft_nms_sigma = nms, float(soft_nms_sigma)
         self.params = _lib.SfaFusionParams(float(conf_threshold), float(fusion_iou_threshold),
-                                           float(nms_threshold), int(mode), 1)
+                                           float(nms_threshold), int(mode), 1 if nms == "greedy" else 0)
         self.proj_params = _lib.SfaProjectParams(0.3, int(conf_source),
                                                  1 if len(calibs) == batch and batch > 1 else 0)
         self.post_prm = post_params()
@@ -682,9 +726,9 @@ class FusionPipeline:
             self.fcount = torch.empty(batch, dtype=i32, device=dev)
             self.fkeep = torch.empty(cap, dtype=i32, device=dev)
             self.fkeep_count = torch.empty(batch, dtype=i32, device=dev)
+            self.fstart = torch.zeros(batch, dtype=i32, device=dev)  # frame b's fused list start
         self.max_camera_boxes = max_camera_boxes
         self.graph = None
-        self.infer_graph = None  # forward + decode only (capture_infer): the BEV stays eager
 
     def set_points(self, clouds):
         self.det.set_points(clouds)
@@ -729,6 +773,10 @@ class FusionPipeline:
                                     self.fcls.data_ptr(), self.fsrc.data_ptr(), None, None,
                                     self.fcount.data_ptr(), self.fkeep.data_ptr(),
                                     self.fkeep_count.data_ptr(), st), "sfa_fuse_detections")
+        if self.nms == "gaussian":
+            torch.add(self.yoff[:-1], self.soff[:-1], out=self.fstart)  # on the current stream (= st)
+            check(L.sfa_gaussian_nms(self.B, self.fbox.data_ptr(), self.fconf.data_ptr(), self.fstart.data_ptr(),
+                                     self.fcount.data_ptr(), self.soft_nms_sigma, st), "sfa_gaussian_nms")
         return self.fcount
 
     def capture(self):
@@ -744,22 +792,6 @@ class FusionPipeline:
             self.graph = g
         return g
 
-    def capture_infer(self):
-        """Capture the forward + decode (everything after the BEV) into a HIP graph that run()
-        replays: the voxeliser's launches depend on the batch's host frame offsets (a new
-        ragged batch per step when streaming), the rest of the step does not."""
-        with torch.cuda.device(self.dev):
-            s = torch.cuda.Stream()
-            s.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(s):
-                self._infer(_lib.stream_ptr(self.dev))  # warm outside capture
-            torch.cuda.current_stream().wait_stream(s)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._infer(_lib.stream_ptr(self.dev))
-            self.infer_graph = g
-        return g
-
     def replay(self):
         if self.graph is None:
             return self.run()
@@ -767,7 +799,8 @@ class FusionPipeline:
         return self.fcount
 
     def results(self):
-        """Host copy per frame: (fused boxes, conf, cls, source, NMS keep indices)."""
+        """Host copy per frame: (fused boxes, conf, cls, source, NMS keep indices); with
+        nms="gaussian" conf is the decayed confidence and keep is every index (nothing dropped)."""
         yoff = self.yoff.cpu().numpy()
         soff = self.soff.cpu().numpy()
         cnt, kc = self.fcount.cpu().numpy(), self.fkeep_count.cpu().numpy()
@@ -777,6 +810,6 @@ class FusionPipeline:
         for b in range(self.B):
             base = yoff[b] + soff[b]
             n = int(cnt[b])
-            out.append((fb[base:base + n], fc[base:base + n], fk[base:base + n], fs[base:base + n],
-                        keep[base:base + int(kc[b])]))
+            kp = np.arange(max(n, 0), dtype=keep.dtype) if self.nms == "gaussian" else keep[base:base + int(kc[b])]
+            out.append((fb[base:base + n], fc[base:base + n], fk[base:base + n], fs[base:base + n], kp))
         return out

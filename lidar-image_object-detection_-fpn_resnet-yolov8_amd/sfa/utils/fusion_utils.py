@@ -5,7 +5,9 @@ The reference keeps these functions inside its scripts (which import ultralytics
 here they live in one module with the same names, arguments and dict outputs:
 ``{'box', 'confidence', 'class_id', 'class_name', 'model', 'color'}``.  The
 association, fusion and NMS run as one wavefront per frame on the GPU, bit-identical
-to the Python loops; ``fuse_frames`` batches many frames in one launch.
+to the Python loops; ``fuse_frames`` batches many frames in one launch.  ``gaussian_nms``
+is the Gaussian soft-NMS of the reference README (README.md:250-261; no reference script
+defines it).
 """
 
 from __future__ import annotations
@@ -82,6 +84,27 @@ def apply_nms_to_fused_detections(detections, nms_threshold=0.5):
     res = runtime.fuse_frames([(np.zeros((0, 4)), np.zeros(0), np.zeros(0), boxes, conf)],
                               -np.inf, 2.0, nms_threshold, _lib.FUSE_BAYES, apply_nms=True)[0]
     return [detections[int(i)] for i in res.keep]
+
+
+def gaussian_nms(detections, sigma=0.5):
+    """README.md:250-261 gaussian_nms (Gaussian soft-NMS): for i in order, every later detection's
+    confidence decays by exp(-iou**2 / sigma), in place; order and boxes unchanged, nothing is
+    dropped. Detections are the fusion dicts (``'box'`` [x, y, w, h], ``'confidence'``) or objects
+    with ``.box`` / ``.confidence`` (the README's attribute form); IoU is calculate_iou
+    (test6.py:76-101). Runs on the GPU (sfa_gaussian_nms); returns ``detections``."""
+    if len(detections) == 0:
+        return detections
+    as_dict = isinstance(detections[0], dict)
+    get = (lambda d, k: d[k]) if as_dict else (lambda d, k: getattr(d, k))
+    boxes = np.array([get(d, "box") for d in detections], np.int64).reshape(-1, 4)
+    conf = np.array([get(d, "confidence") for d in detections], np.float64)
+    out = runtime.gaussian_nms_frames([(boxes, conf)], sigma)[0]
+    for d, c in zip(detections, out):
+        if as_dict:
+            d["confidence"] = float(c)
+        else:
+            d.confidence = float(c)
+    return detections
 
 
 def _fuse_dicts(yolov8_detections, sfa3d_detections, thr, mode):

@@ -14,9 +14,16 @@ how they were run):
   fuse_inputs        test6.py:310-348 / test5.py:285-321: the conf >= threshold filter
   nms                test6.py:104-126: stable sort by confidence (descending), greedy,
                      suppress when IoU > threshold
+  gaussian_nms       README.md:250-261 (the reference's only definition of it; no script
+                     implements it): for i in order, every later detection j decays,
+                     conf_j *= np.exp(-iou**2 / sigma); nothing is re-sorted or dropped
+                     (pinned by tests/golden/gen_gaussian_nms_golden.py, which runs the
+                     README's own snippet)
 """
 
 from __future__ import annotations
+
+import numpy as np
 
 YOLO, SFA, FUSED = 0, 1, 2
 
@@ -96,3 +103,14 @@ def run(case, mode):
                          case["sfa_boxes"], case["sfa_conf"], case["conf_thr"])
     fused = associate_fuse(ys, ss, case["fusion_iou"], mode)
     return fused, nms(fused, case["nms_thr"])
+
+
+def gaussian_nms(boxes, conf, sigma=0.5):
+    """README.md:250-261 on one frame: boxes [[x, y, w, h], ...], conf f64 -> decayed conf (list)."""
+    c = [np.float64(v) for v in conf]
+    n = len(c)
+    for i in range(n):
+        for j in range(i + 1, n):
+            v = iou(boxes[i], boxes[j])
+            c[j] = c[j] * np.exp(-v ** 2 / sigma)
+    return [float(v) for v in c]

@@ -41,6 +41,16 @@ def golden_fusion():
 
 
 @pytest.fixture(scope="session")
+def golden_gaussian_nms():
+    import numpy as np
+    return np.load(os.path.join(GOLDEN, "gaussian_nms_golden.npz"))
+
+
+def gaussian_nms_case_names(g):
+    return sorted({k.split("/")[0] for k in g.files})
+
+
+@pytest.fixture(scope="session")
 def golden_back():
     import numpy as np
     return np.load(os.path.join(GOLDEN, "back_golden.npz"))

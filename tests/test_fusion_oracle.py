@@ -31,3 +31,15 @@ def test_iou_matrix(golden_fusion, name):
     m = np.array([[fo.iou(a, b) for b in case["sfa_boxes"]] for a in case["yolo_boxes"]],
                  np.float64).reshape(len(case["yolo_boxes"]), len(case["sfa_boxes"]))
     np.testing.assert_array_equal(m, golden_fusion[f"{name}/iou"])
+
+
+def test_gaussian_nms_oracle_matches_readme_snippet(golden_gaussian_nms):
+    """oracle.gaussian_nms == the README's gaussian_nms (README.md:250-261) as run by
+    tests/golden/gen_gaussian_nms_golden.py, bit for bit (same numpy exp)."""
+    from conftest import gaussian_nms_case_names
+    g = golden_gaussian_nms
+    names = gaussian_nms_case_names(g)
+    assert len(names) >= 9
+    for name in names:
+        got = fo.gaussian_nms(g[f"{name}/boxes"].tolist(), g[f"{name}/conf_in"], float(g[f"{name}/sigma"]))
+        np.testing.assert_array_equal(np.array(got, np.float64), g[f"{name}/conf_out"], err_msg=name)

@@ -102,3 +102,40 @@ def test_dict_api_matches_reference(golden_fusion, gpu):
     out = fu.fuse_overlapping_detections(ydicts, sdicts, c["fusion_iou"])
     np.testing.assert_array_equal(np.array([d["box"] for d in out]), g["low_fusion_thr/weighted/box"])
     assert fu.calculate_iou([0, 0, 10, 10], [5, 0, 10, 10]) == fo.iou([0, 0, 10, 10], [5, 0, 10, 10])
+
+
+def test_gaussian_nms_matches_readme_snippet(golden_gaussian_nms, gpu):
+    """sfa_gaussian_nms (all golden cases as frames of one launch) vs the README's gaussian_nms:
+    the same products in the same order, so only the f64 exp of the device vs numpy can differ
+    (last bit): relative tolerance 1e-14; boxes / order / count untouched by definition."""
+    from conftest import gaussian_nms_case_names
+    g = golden_gaussian_nms
+    names = gaussian_nms_case_names(g)
+    for sigma in sorted({float(g[f"{n}/sigma"]) for n in names}):
+        sel = [n for n in names if float(g[f"{n}/sigma"]) == sigma]
+        got = runtime.gaussian_nms_frames([(g[f"{n}/boxes"], g[f"{n}/conf_in"]) for n in sel], sigma, device=gpu)
+        for n, c in zip(sel, got):
+            ref = g[f"{n}/conf_out"]
+            assert c.shape == ref.shape, n
+            np.testing.assert_allclose(c, ref, rtol=1e-14, atol=0, err_msg=n)
+
+
+def test_gaussian_nms_dropin_dicts_and_objects(golden_gaussian_nms, gpu):
+    """utils.fusion_utils.gaussian_nms on the fusion dicts and on attribute objects (the
+    README's form): in place, same order, same boxes."""
+    from utils.fusion_utils import gaussian_nms
+    g = golden_gaussian_nms
+    boxes, conf = g["random130_sigma03/boxes"], g["random130_sigma03/conf_in"]
+    ref = g["random130_sigma03/conf_out"]
+    dets = [{"box": b.tolist(), "confidence": float(c), "class_id": 0} for b, c in zip(boxes, conf)]
+    assert gaussian_nms(dets, sigma=0.3) is dets
+    np.testing.assert_allclose([d["confidence"] for d in dets], ref, rtol=1e-14, atol=0)
+    assert [d["box"] for d in dets] == boxes.tolist()
+
+    class D:
+        def __init__(self, b, c):
+            self.box, self.confidence = b, c
+    objs = [D(b.tolist(), float(c)) for b, c in zip(boxes, conf)]
+    gaussian_nms(objs, sigma=0.3)
+    np.testing.assert_allclose([o.confidence for o in objs], ref, rtol=1e-14, atol=0)
+    assert gaussian_nms([], 0.5) == []

@@ -16,8 +16,11 @@ from sfa_hip import _lib, runtime, synthetic
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("conf_source", [_lib.CONF_CLASS_ID, _lib.CONF_SCORE])
-def test_fusion_pipeline_matches_oracles(golden, gpu, conf_source):
+@pytest.mark.parametrize("conf_source,nms", [(_lib.CONF_CLASS_ID, "greedy"), (_lib.CONF_SCORE, "greedy"),
+                                             (_lib.CONF_SCORE, "gaussian")])
+def test_fusion_pipeline_matches_oracles(golden, gpu, conf_source, nms):
+    """nms="gaussian": the README's Gaussian soft-NMS (README.md:250-261) on the fused lists
+    instead of the greedy NMS: confidences within 1e-14 rel. of the oracle (device vs numpy exp)."""
     B = 4
     arch = _lib.make_arch(gc.HEADS)
     eng = runtime.KfpnEngine(arch, runtime.pack_state_dict(gc.state_dict_np(golden.model), arch), gpu)
@@ -27,7 +30,7 @@ def test_fusion_pipeline_matches_oracles(golden, gpu, conf_source):
               for n in names]
     clouds = [synthetic.synthetic_point_cloud(s) for s in range(1, B + 1)]
     fp = runtime.FusionPipeline(eng, B, calibs, K=50, max_points=sum(c.shape[0] for c in clouds),
-                                conf_source=conf_source, fusion_iou_threshold=0.3)
+                                conf_source=conf_source, fusion_iou_threshold=0.3, nms=nms, soft_nms_sigma=0.5)
     fp.set_points(clouds)
     # camera boxes: jittered copies of the first pass's projected boxes + random extras
     fp.set_camera([(np.zeros((0, 4)), np.zeros(0), np.zeros(0))] * B)
@@ -65,9 +68,14 @@ def test_fusion_pipeline_matches_oracles(golden, gpu, conf_source):
         fused, keep = fo.run(case, "bayes")
         gb, gconf, gcls, gsrc, gkeep = res[b]
         np.testing.assert_array_equal(gb, np.array([f[0] for f in fused], np.int64).reshape(-1, 4))
-        np.testing.assert_array_equal(gconf, np.array([f[1] for f in fused]))
         np.testing.assert_array_equal(gsrc, np.array([f[3] for f in fused]))
-        np.testing.assert_array_equal(gkeep, np.array(keep))
+        if nms == "gaussian":
+            ref = fo.gaussian_nms([f[0] for f in fused], [f[1] for f in fused], 0.5)
+            np.testing.assert_allclose(gconf, np.array(ref, np.float64).reshape(-1), rtol=1e-14, atol=0)
+            np.testing.assert_array_equal(gkeep, np.arange(len(fused)))
+        else:
+            np.testing.assert_array_equal(gconf, np.array([f[1] for f in fused]))
+            np.testing.assert_array_equal(gkeep, np.array(keep))
         n_fused += int(np.sum(gsrc == _lib.SRC_FUSED))
     if conf_source == _lib.CONF_SCORE:
         assert n_fused > 0
