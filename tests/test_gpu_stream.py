@@ -31,7 +31,10 @@ def test_device_stream_matches_fromfile(tmp_path, gpu):
         assert i == len(paths)
 
 
-def test_streaming_detector_matches_pipeline(tmp_path, golden, gpu):
+@pytest.mark.parametrize("inflight,graph", [(1, True), (1, False), (2, True)])
+def test_streaming_detector_matches_pipeline(tmp_path, golden, gpu, inflight, graph):
+    """Every configuration (forward + decode as a HIP graph or eager; 1 or 2 pipelines in flight,
+    the second on a twin model handle over the same weights) == the eager resident pipeline."""
     clouds = [synthetic.synthetic_point_cloud(s) for s in range(1, 6)]  # 5 frames, batch 2
     paths = []
     for i, c in enumerate(clouds):
@@ -41,7 +44,7 @@ def test_streaming_detector_matches_pipeline(tmp_path, golden, gpu):
     arch = _lib.make_arch(gc.HEADS)
     eng = runtime.KfpnEngine(arch, runtime.pack_state_dict(gc.state_dict_np(golden.model), arch), gpu)
     got = []
-    sd = StreamingDetector(eng, paths, batch=2, K=50, n_threads=2)
+    sd = StreamingDetector(eng, paths, batch=2, K=50, n_threads=2, inflight=inflight, graph=graph)
     sd.run(lambda dets, n, k: got.append(dets[:n].clone()))
     torch.cuda.synchronize()
     sd.close()
