@@ -66,7 +66,8 @@ static bool strip_ok(const ConvArgs& a) {
 //    profiles/r02_convbench_*.txt). SFA_TUNE bits 4 / 8 / 16 return the heads / the big-M
 //    non-strip convs / the strip convs to the round-1 kernels for same-box A/B, bit 32 the FPN
 //    skip convs, bit 64 the heads to the unpacked epilogue, bit 128 the 64-wide strip convs to
-//    no residual prefetch, bit 256 the conv_r3 launches to the tap-major K order;
+//    no residual prefetch, bit 256 the conv_r3 launches to the tap-major K order, bit 512 the
+//    128..512-wide conv_h3 launches to the 32x32x16 MFMA form;
 //  * split-K 2 for the 512-wide (layer4) convs, whose 184 tiles cannot fill 256 CUs (-13..16 %);
 //    picked from the width only, so a frame's arithmetic never depends on the batch.
 // conv_x6g_kernel<..., PREC 1> tiles as the fallback.
@@ -149,7 +150,14 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
       else
         rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
     }
-    if (!ok(rc)) rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
+    if (!ok(rc)) {
+      // 16x16x32 MFMA form (round 2): -6 % per launch on layer3.0.conv1, +1.2 % end to end
+      // (profiles/r02_ab_h3_mf1.txt); SFA_TUNE bit 512 returns to the 32x32x16 form
+      if (tune_flags() & 512)
+        rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
+      else
+        rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2, 1>(b, st);
+    }
     if (!ok(rc) && b.ksplit > 1) {  // K not divisible into the slices: no split
       b.ksplit = 1;
       if (strip) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);

@@ -286,7 +286,7 @@ def test_round2_kernels_match_round1(golden, gpu, monkeypatch, hw):
         assert e <= 1e-4, h
 
 
-@pytest.mark.parametrize("tune", ["0", "28", "32", "256"])
+@pytest.mark.parametrize("tune", ["0", "28", "32", "256", "512"])
 def test_batch_invariance_608(golden, gpu, monkeypatch, tune):
     """At the full 608x608 size (every kernel path of the bench: r3 heads, strip convs, FPN skip
     convs, r3 body convs (M >= 50000 needs >= 9 frames), split-K layer4): frames 7, 8 of a batch

@@ -256,16 +256,17 @@ int main(int argc, char** argv) {
   };
   // round 2: conv_r3_kernel (A in registers) against the round-1 defaults (first entry of each)
   std::vector<Cand> n64 = {
-      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDR(256, 64, 32, EPI_STD, 2, 2, 554752, 1),
-      CANDR(128, 64, 32, EPI_STD, 4, 2, 554752, 1), CANDR(256, 64, 64, EPI_STD, 2, 2, 554752, 1),
-      CANDR(128, 64, 32, EPI_STD, 4, 2, 546560, 1),
+      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDR(256, 64, 32, EPI_STD, 2, 2, 555264, 1),
+      CANDR(128, 64, 32, EPI_STD, 4, 2, 555264, 1), CANDR(256, 64, 64, EPI_STD, 2, 2, 555264, 1),
+      CANDR(128, 64, 32, EPI_STD, 4, 2, 547072, 1),
   };
   std::vector<Cand> stem = {
       CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
   };
   std::vector<Cand> nbig = {
-      CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDR(128, 128, 32, EPI_STD, 2, 2, 554752, 1),
-      CANDR(128, 128, 32, EPI_STD, 2, 2, 546560, 1), CANDR(256, 128, 32, EPI_STD, 1, 2, 554752, 1),
+      CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDK(128, 128, 32, EPI_STD, 2, 2, 2, 0, 1),
+      CANDK(128, 128, 32, EPI_STD, 2, 2, 2, 1, 1), CANDK(128, 128, 32, EPI_STD, 2, 2, 0, 1, 1),
+      CANDK(128, 128, 32, EPI_STD, 2, 2, 2, 0, 1), CANDK(128, 128, 32, EPI_STD, 2, 2, 2, 1, 1),
   };
   std::vector<Cand> heads = {
       CANDR(256, 320, 32, EPI_HEAD, 1, 2, 620804, 1), CANDR(128, 320, 32, EPI_HEAD, 2, 2, 620804, 1),
