@@ -43,9 +43,11 @@ constexpr int LDS_BYTES = W_BYTES + 2 * PATCH_TERM + T_BYTES;  // 151,600 B: one
 // cells with one writer (j, i in 1..7) are stored, the tile-border cells combined by
 // atomicMax on the f32 bits (values >= +0) into the zeroed pooled buffer, as
 // h3_pool_epilogue does. NOATOM (ablation ABL 16) applies to the A/B form only.
-template <bool NOATOM = false>
-__device__ __forceinline__ void stem_pool_epilogue(const ConvArgs& a, x6_f32x16 (&acc)[1][2], float* T, int b,
-                                                   int th, int tw, int wave, int tid, float ainv) {
+// ReLU(conv * 1/s * winv + b) of the wave's 32 rows into the tile T (row = 32 wave + q, q the
+// row within the wave: pixel (2 wave + q / 16, q % 16)), returns the lane's max. One rounding
+// (fmaf) per value, in both accumulator forms.
+__device__ __forceinline__ float stem_tile_store32(const ConvArgs& a, x6_f32x16 (&acc)[1][2], float* T, int wave,
+                                                   int tid, float ainv) {
   constexpr int LD = 68;
   const int lane = tid & 63, r = lane & 31, h = lane >> 5;
   float mx = 0.f;
@@ -57,12 +59,45 @@ __device__ __forceinline__ void stem_pool_epilogue(const ConvArgs& a, x6_f32x16 
 #pragma unroll
     for (int v = 0; v < 16; ++v) {
       const int row = wave * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-      float val = acc[0][ni][v] * cs + bn;
+      float val = fmaf(acc[0][ni][v], cs, bn);
       val = val > 0.f ? val : 0.f;
       T[row * LD + n] = val;
       mx = fmaxf(mx, val);
     }
   }
+  return mx;
+}
+// The same for the 16x16x32 form (acc[mi][ni]: lane l, register v -> row 16 mi + 4 (l >> 4) + v of
+// the wave's 32, channel 16 ni + (l & 15); row stride 68 floats keeps the four row groups of a
+// store on distinct banks).
+__device__ __forceinline__ float stem_tile_store16(const ConvArgs& a, f32x4_t (&acc)[2][4], float* T, int wave, int tid,
+                                                   float ainv) {
+  constexpr int LD = 68;
+  const int lane = tid & 63, c16 = lane & 15, g = lane >> 4;
+  float mx = 0.f;
+#pragma unroll
+  for (int ni = 0; ni < 4; ++ni) {
+    const int n = ni * 16 + c16;
+    const float bn = a.bias[n];
+    const float cs = a.winv[n] * ainv;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int row = wave * 32 + 16 * mi + 4 * g + v;
+        float val = fmaf(acc[mi][ni][v], cs, bn);
+        val = val > 0.f ? val : 0.f;
+        T[row * LD + n] = val;
+        mx = fmaxf(mx, val);
+      }
+  }
+  return mx;
+}
+
+template <bool NOATOM = false>
+__device__ __forceinline__ void stem_pool_epilogue(const ConvArgs& a, float mx, float* T, int b, int th, int tw,
+                                                   int tid) {
+  constexpr int LD = 68;
   if (a.amax_out)
     amax_commit_block<8>(a.amax_out, b, mx, 0.f, T + 256 * LD);  // includes __syncthreads
   else
@@ -142,10 +177,12 @@ __global__ void __launch_bounds__(256) stem_pool_merge_kernel(const ConvArgs a, 
 
 // ABL (timing ablations only, env SFA_STEM_ABL; results wrong): 1 = no epilogue, 2 = no MFMAs,
 // 4 = no patch fetch, 8 = first patch fetched after the weights are staged,
-// 16 = border cells stored instead of atomicMax (only with a.part == null: the atomic A/B form)
+// 16 = border cells stored instead of atomicMax (only with a.part == null: the atomic A/B form),
+// 64 = the 32x32x16 MFMA form (round 1) instead of 16x16x32 (same products, other summation order)
 template <int ABL = 0>
 __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs a, int ntiles) {
   using namespace stem_patch;
+  constexpr bool M16 = (ABL & 64) == 0;  // 16x16x32 MFMAs (default); ABL 64: the 32x32x16 form
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
   unsigned char* SW = smem;
   unsigned char* SU = smem + W_BYTES;                   // patch, 2 terms
@@ -222,39 +259,77 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs 
     lds_barrier();
     if (tile + (int)gridDim.x < ntiles && !(ABL & 4)) fetch(tile + gridDim.x);  // lands during the MFMAs
 
-    x6_f32x16 acc[1][2];
+    float mx;
+    if constexpr (M16) {
+      // 16x16x32: k-step s = kh (32 k = kw 0..7 x c 0..3); lane (row l & 15, k-group g = l >> 4)
+      // holds kw 2g, 2g + 1 of its row's pixel = one 16-B patch read per term; 2 row blocks
+      // (conv rows 2 wave, 2 wave + 1) x 4 column blocks x 3 products per k-step
+      f32x4_t acc[2][4];
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
+      for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-      for (int v = 0; v < 16; ++v) acc[0][ni][v] = 0.f;
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      const int c16 = lane & 15, g4 = lane >> 4;
+      const int abase16 = ((2 * (2 * wave)) * PW + 2 * c16 + 2 * g4) * 8;  // row block 0: conv row 2 wave
+      const int bbase16 = c16 * WROW + 16 * g4;
 #pragma unroll
-    for (int s = 0; s < ((ABL & 2) ? 0 : KP / 16); ++s) {
-      const int aoff = abase + ((s >> 1) * PW + 4 * (s & 1)) * 8;
-      const f16x8_t ahi = *reinterpret_cast<const f16x8_t*>(SU + aoff);
-      const f16x8_t alo = *reinterpret_cast<const f16x8_t*>(SU + PATCH_TERM + aoff);
+      for (int s = 0; s < ((ABL & 2) ? 0 : KP / 32); ++s) {
+        f16x8_t ahi[2], alo[2];
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
-        const unsigned char* wb = SW + bbase + ni * 32 * WROW + 32 * s;
-        const f16x8_t whi = *reinterpret_cast<const f16x8_t*>(wb);
-        const f16x8_t wlo = *reinterpret_cast<const f16x8_t*>(wb + 64 * WROW);
-        x6_f32x16 cc = acc[0][ni];
-        cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi, cc, 0, 0, 0);
-        cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo, cc, 0, 0, 0);
-        cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi, cc, 0, 0, 0);
-        acc[0][ni] = cc;
+        for (int mi = 0; mi < 2; ++mi) {
+          const int aoff = abase16 + (2 * mi * PW + s * PW) * 8;  // conv row + mi -> patch row + 2 mi
+          ahi[mi] = *reinterpret_cast<const f16x8_t*>(SU + aoff);
+          alo[mi] = *reinterpret_cast<const f16x8_t*>(SU + PATCH_TERM + aoff);
+        }
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const unsigned char* wb = SW + bbase16 + ni * 16 * WROW + 64 * s;
+          const f16x8_t whi = *reinterpret_cast<const f16x8_t*>(wb);
+          const f16x8_t wlo = *reinterpret_cast<const f16x8_t*>(wb + 64 * WROW);
+#pragma unroll
+          for (int mi = 0; mi < 2; ++mi) {
+            f32x4_t cc = acc[mi][ni];
+            cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[mi], whi, cc, 0, 0, 0);
+            cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[mi], wlo, cc, 0, 0, 0);
+            cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[mi], whi, cc, 0, 0, 0);
+            acc[mi][ni] = cc;
+          }
+        }
       }
+      mx = stem_tile_store16(a, acc, reinterpret_cast<float*>(ST), wave, tid, ainv[0]);
+    } else {
+      x6_f32x16 acc[1][2];
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int v = 0; v < 16; ++v) acc[0][ni][v] = 0.f;
+#pragma unroll
+      for (int s = 0; s < ((ABL & 2) ? 0 : KP / 16); ++s) {
+        const int aoff = abase + ((s >> 1) * PW + 4 * (s & 1)) * 8;
+        const f16x8_t ahi = *reinterpret_cast<const f16x8_t*>(SU + aoff);
+        const f16x8_t alo = *reinterpret_cast<const f16x8_t*>(SU + PATCH_TERM + aoff);
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          const unsigned char* wb = SW + bbase + ni * 32 * WROW + 32 * s;
+          const f16x8_t whi = *reinterpret_cast<const f16x8_t*>(wb);
+          const f16x8_t wlo = *reinterpret_cast<const f16x8_t*>(wb + 64 * WROW);
+          x6_f32x16 cc = acc[0][ni];
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(alo, whi, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, wlo, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ahi, whi, cc, 0, 0, 0);
+          acc[0][ni] = cc;
+        }
+      }
+      mx = stem_tile_store32(a, acc, reinterpret_cast<float*>(ST), wave, tid, ainv[0]);
     }
     // the epilogue's own barrier (after its ST writes) also orders this tile's patch reads
     // before the next tile's patch stores
     if constexpr ((ABL & 1) != 0) {
-      float t = 0.f;
-#pragma unroll
-      for (int v = 0; v < 16; ++v) t += acc[0][0][v] + acc[0][1][v];
-      if (t == 1234.5f) a.y[tid] = t;
+      if (mx == 1234.5f) a.y[tid] = mx;
       __syncthreads();
     } else {
       const int tl = tile - b * tiles_per_frame, th = tl / tw_n;
-      stem_pool_epilogue<(ABL & 16) != 0>(a, acc, reinterpret_cast<float*>(ST), b, th, tl - th * tw_n, wave, tid, ainv[0]);
+      stem_pool_epilogue<(ABL & 16) != 0>(a, mx, reinterpret_cast<float*>(ST), b, th, tl - th * tw_n, tid);
     }
   }
 }
@@ -293,6 +368,7 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
     case 3: hipLaunchKernelGGL(stem_patch_pool_kernel<3>, gd, bd, 0, st, a, ntiles); break;
     case 8: hipLaunchKernelGGL(stem_patch_pool_kernel<8>, gd, bd, 0, st, a, ntiles); break;
     case 16: hipLaunchKernelGGL(stem_patch_pool_kernel<16>, gd, bd, 0, st, a, ntiles); break;
+    case 64: hipLaunchKernelGGL(stem_patch_pool_kernel<64>, gd, bd, 0, st, a, ntiles); break;
     default: hipLaunchKernelGGL(stem_patch_pool_kernel<0>, gd, bd, 0, st, a, ntiles); break;
   }
   SFA_LAUNCH_CHECK();
