@@ -90,6 +90,9 @@ def parse():
                          "(README.md:250-261)")
     ap.add_argument("--stream-inflight", type=int, default=1,
                     help="--workload stream: pipelines in flight (profiles/r02_stream_variants.txt)")
+    ap.add_argument("--share-weights", action="store_true",
+                    help="the in-flight pipelines share one device copy of the packed weights "
+                         "(KfpnEngine.twin) instead of one copy each")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--serial-heads", action="store_true",
                     help="keep the level-0 heads on the main stream (no side stream) for the whole "
@@ -121,12 +124,13 @@ def init_dist(n):
     return rank, world, torch.device("cuda", local)
 
 
-def build_pipeline(dev, args, rank):
-    arch = _lib.make_arch(DEFAULT_HEADS)
-    spec = _lib.state_layout(arch)
-    sd = synthetic.synthetic_state_dict(spec, seed=0)
-    engine = KfpnEngine(arch, pack_state_dict(sd, arch), dev,
-                        math=MATHS[args.math])
+def build_pipeline(dev, args, rank, engine=None):
+    if engine is None:
+        arch = _lib.make_arch(DEFAULT_HEADS)
+        spec = _lib.state_layout(arch)
+        sd = synthetic.synthetic_state_dict(spec, seed=0)
+        engine = KfpnEngine(arch, pack_state_dict(sd, arch), dev,
+                            math=MATHS[args.math])
     if args.workload == "e2e":
         clouds = [synthetic.synthetic_point_cloud(1000 * rank + i + 1) for i in range(args.batch)]
         pipe = DetectorPipeline(engine, args.batch, K=args.K, with_bev=True,
@@ -373,27 +377,41 @@ def run_fusion(args, rank, world, dev):
     cal = project_cases.calibs()["avg"]
     calib = runtime_make_calib(cal)
     clouds = [synthetic.synthetic_point_cloud(1000 * rank + i + 1) for i in range(args.batch)]
-    fp = FusionPipeline(engine, args.batch, [calib], K=args.K, nms=args.fusion_nms,
-                        max_points=sum(c.shape[0] for c in clouds), conf_source=_lib.CONF_SCORE)
-    fp.set_points(clouds)
     cams = []
     for i in range(args.batch):
         u = synthetic.hash_uniform(77, i, 30 * 6).reshape(30, 6)
         boxes = np.stack([u[:, 0] * 1150, u[:, 1] * 320, 10 + u[:, 2] * 120, 10 + u[:, 3] * 90], 1)
         cams.append((boxes.astype(np.int64), u[:, 4].astype(np.float32).astype(np.float64),
                      (u[:, 5] * 80).astype(np.int64)))
-    fp.set_camera(cams)
-    if not args.no_graph:
-        fp.capture()
-    for _ in range(args.warmup):
-        fp.replay()
+    # --inflight pipelines (each with its own model handle and buffers) replayed on their own
+    # streams in turn, as in the bev_infer workload: one step's kernel tails and its small
+    # latency-bound post-processing / fusion launches overlap the other step's convolutions
+    nf = max(1, args.inflight)
+    fps = []
+    for i in range(nf):
+        fp = FusionPipeline(engine if i == 0 else engine.twin(), args.batch, [calib], K=args.K,
+                            nms=args.fusion_nms, max_points=sum(c.shape[0] for c in clouds),
+                            conf_source=_lib.CONF_SCORE)
+        fp.set_points(clouds)
+        fp.set_camera(cams)
+        if not args.no_graph:
+            fp.capture()
+        fps.append(fp)
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nf - 1)]
+
+    def step(k):
+        with torch.cuda.stream(streams[k % nf]):
+            fps[k % nf].replay()
+
+    for k in range(args.warmup):
+        step(k)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        fp.replay()
+    for k in range(args.steps):
+        step(k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -435,7 +453,7 @@ def main():
                                    "decode K=%d -> post_process -> camera boxes -> Bayesian "
                                    "fusion + %s NMS, bs=%d per GPU, one HIP graph"
                                    % (args.K, args.fusion_nms, args.batch),
-                       "global_batch": world * args.batch}
+                       "global_batch": world * args.batch, "steps_in_flight": max(1, args.inflight)}
             print(json.dumps({
                 "metric": METRIC, "value": round(frames / elapsed, 2), "unit": "frames/s",
                 "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -448,7 +466,9 @@ def main():
             dist.destroy_process_group()
         return
     nf = max(1, args.inflight)
-    pipes = [build_pipeline(dev, args, rank) for _ in range(nf)]
+    pipes = [build_pipeline(dev, args, rank)]
+    for _ in range(nf - 1):  # own model handle each; weights shared (--share-weights) or a copy each
+        pipes.append(build_pipeline(dev, args, rank, pipes[0].engine.twin() if args.share_weights else None))
     if args.serial_heads:
         for p in pipes:
             p.engine.set_probe(_lib.PROBE_SERIAL)
