@@ -88,8 +88,9 @@ def parse():
     ap.add_argument("--fusion-nms", choices=["greedy", "gaussian"], default="greedy",
                     help="--workload fusion: test6.py's greedy NMS or the README's Gaussian soft-NMS "
                          "(README.md:250-261)")
-    ap.add_argument("--stream-inflight", type=int, default=1,
-                    help="--workload stream: pipelines in flight (profiles/r02_stream_variants.txt)")
+    ap.add_argument("--stream-inflight", type=int, default=2,
+                    help="--workload stream: pipelines in flight; with 2+ the engines run without "
+                         "side streams (profiles/r02b_stream_side_streams.txt)")
     ap.add_argument("--share-weights", action="store_true",
                     help="the in-flight pipelines share one device copy of the packed weights "
                          "(KfpnEngine.twin) instead of one copy each")
@@ -330,8 +331,10 @@ def run_stream(args, rank, world, dev):
     from sfa_hip.stream import StreamingDetector
     arch = _lib.make_arch(DEFAULT_HEADS)
     sd = synthetic.synthetic_state_dict(_lib.state_layout(arch), seed=0)
+    # several pipelines in flight + the copy stream: no side streams, so every stream keeps a
+    # hardware queue of its own (profiles/r02b_stream_side_streams.txt)
     engine = KfpnEngine(arch, pack_state_dict(sd, arch), dev,
-                        math=MATHS[args.math])
+                        math=MATHS[args.math], side_streams=args.stream_inflight < 2)
     tmp = tempfile.mkdtemp(prefix=f"sfa_bins_r{rank}_", dir="/tmp")
     try:
         files = []
@@ -445,7 +448,8 @@ def main():
                 cfg = {"workload": "KITTI .bin stream -> pinned DMA -> BEV -> fpn_resnet_18 "
                                    "forward -> decode K=%d, bs=%d per GPU (forward + decode as a "
                                    "HIP graph, BEV eager: per-batch frame offsets)" % (args.K, args.batch),
-                       "reader_threads": threads, "global_batch": world * args.batch}
+                       "reader_threads": threads, "global_batch": world * args.batch,
+                       "steps_in_flight": max(1, args.stream_inflight)}
             else:
                 data = ("synthetic 132,880-pt sweeps + 30 synthetic camera boxes per frame "
                         "(YOLOv8n itself not in the framework)")

@@ -124,6 +124,15 @@ typedef struct sfa_model sfa_model;
 int sfa_model_create(const sfa_arch* arch, const float* packed_device, sfa_model** out);
 void sfa_model_destroy(sfa_model* model);
 
+/* Side streams on (1, the default; env SFA_SIDE_STREAMS=0 at create time turns them off) or
+ * off (0: every launch of the forward on the caller's stream).  Off destroys them (after their
+ * last forward has finished), on creates them on the current device.  Every stream of a
+ * process takes one of HIP's hardware queues (4 by default), so a caller running several
+ * forwards in flight beside a copy stream turns them off (the KITTI .bin stream workload:
+ * profiles/r02b_stream_side_streams.txt).  Not concurrently with a forward of this model.
+ * No reference counterpart (measurement / scheduling). */
+int sfa_model_set_side_streams(sfa_model* model, int on);
+
 /* Arithmetic of the convolutions (all results are f32; every mode meets the parity
  * bar):
  *   SFA_MATH_FP16X3 (default) — operands scaled by powers of two (weights per output channel at

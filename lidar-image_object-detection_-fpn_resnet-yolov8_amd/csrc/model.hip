@@ -309,6 +309,34 @@ struct sfa_model {
   hipEvent_t probe_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
 };
 
+// The model's side stream(s) and their events, created on the current device; on failure
+// (no device) none, and the forward runs every launch on the caller's stream.
+static void drop_side_streams(sfa_model* m) {
+  for (hipEvent_t* e : {&m->fork, &m->join, &m->mid, &m->join2})
+    if (*e) {
+      (void)hipEventDestroy(*e);
+      *e = nullptr;
+    }
+  for (hipStream_t* s : {&m->side2, &m->side})
+    if (*s) {
+      (void)hipStreamDestroy(*s);
+      *s = nullptr;
+    }
+}
+
+static void make_side_streams(sfa_model* m) {
+  if (hipGetDevice(&m->device) != hipSuccess ||
+      hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&m->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&m->join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&m->mid, hipEventDisableTiming) != hipSuccess ||
+      (m->fpn3_side && (hipStreamCreateWithFlags(&m->side2, hipStreamNonBlocking) != hipSuccess ||
+                        hipEventCreateWithFlags(&m->join2, hipEventDisableTiming) != hipSuccess))) {
+    (void)hipGetLastError();
+    drop_side_streams(m);
+  }
+}
+
 extern "C" int sfa_abi_version(void) { return SFA_ABI_VERSION; }
 extern "C" const char* sfa_last_error_string(void) { return g_err.c_str(); }
 
@@ -454,17 +482,7 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   if (const char* e = getenv("SFA_FPN3_SIDE")) m->fpn3_side = strcmp(e, "0") != 0;
   bool side_streams = true;  // env SFA_SIDE_STREAMS=0: every launch on the caller's stream (A/B)
   if (const char* e = getenv("SFA_SIDE_STREAMS")) side_streams = strcmp(e, "0") != 0;
-  if (!side_streams || hipGetDevice(&m->device) != hipSuccess ||
-      hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&m->fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&m->join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&m->mid, hipEventDisableTiming) != hipSuccess ||
-      (m->fpn3_side && (hipStreamCreateWithFlags(&m->side2, hipStreamNonBlocking) != hipSuccess ||
-                        hipEventCreateWithFlags(&m->join2, hipEventDisableTiming) != hipSuccess))) {
-    // no device (or no stream): the forward runs every launch on the caller's stream
-    (void)hipGetLastError();
-    m->side = nullptr;
-  }
+  if (side_streams) make_side_streams(m);
   *out = m;
   return SFA_OK;
 }
@@ -473,13 +491,24 @@ extern "C" void sfa_model_destroy(sfa_model* model) {
   if (!model) return;
   for (hipEvent_t e : model->probe_ev)
     if (e) (void)hipEventDestroy(e);
-  if (model->fork) (void)hipEventDestroy(model->fork);
-  if (model->join) (void)hipEventDestroy(model->join);
-  if (model->mid) (void)hipEventDestroy(model->mid);
-  if (model->join2) (void)hipEventDestroy(model->join2);
-  if (model->side2) (void)hipStreamDestroy(model->side2);
-  if (model->side) (void)hipStreamDestroy(model->side);
+  drop_side_streams(model);
   delete model;
+}
+
+extern "C" int sfa_model_set_side_streams(sfa_model* model, int on) {
+  SFA_CHECK_ARG(model, "set_side_streams: null model");
+  std::lock_guard<std::mutex> lk(model->fork_mu);
+  if (!on && model->side) {
+    // the side streams' last forward must be done before they go (the caller's stream has
+    // joined them, so nothing enqueued later depends on them)
+    SFA_HIP_TRY(hipStreamSynchronize(model->side));
+    if (model->side2) SFA_HIP_TRY(hipStreamSynchronize(model->side2));
+    drop_side_streams(model);
+  } else if (on && !model->side) {
+    make_side_streams(model);
+    SFA_CHECK_ARG(model->side, "set_side_streams: no side stream could be created on this device");
+  }
+  return SFA_OK;
 }
 
 extern "C" int sfa_model_set_math(sfa_model* model, int math) {

@@ -77,6 +77,7 @@ _PROTOS["sfa_model_set_math"] = (_c_int, [_vp, _c_int])
 _PROTOS["sfa_model_get_math"] = (_c_int, [_vp])
 PROBE_HEADS, PROBE_SERIAL = 1, 2
 _PROTOS["sfa_model_set_probe"] = (_c_int, [_vp, _c_int])
+_PROTOS["sfa_model_set_side_streams"] = (_c_int, [_vp, _c_int])
 _PROTOS["sfa_model_probe_times"] = (_c_int, [_vp, ctypes.POINTER(ctypes.c_float), _c_int])
 
 

@@ -64,7 +64,7 @@ def pack_state_dict(state: dict, arch) -> np.ndarray:
 class KfpnEngine:
     """A device copy of the packed weights + an sfa_model handle + workspace cache."""
 
-    def __init__(self, arch, packed_host: np.ndarray, device, math=None):
+    def __init__(self, arch, packed_host: np.ndarray, device, math=None, side_streams: bool = True):
         self.arch = arch
         self.device = torch.device(device)
         self.heads = [(arch.head_names[j].value.decode(), int(arch.head_channels[j]))
@@ -76,17 +76,29 @@ class KfpnEngine:
                   "sfa_model_create")
         self._h = h
         self._ws = {}
+        self.side_streams = True
         self.set_math(_lib.math_from_env() if math is None else math)
+        if not side_streams:
+            self.set_side_streams(False)
 
     def set_math(self, math: int):
         """_lib.MATH_FP16X3 (default), _lib.MATH_BF16X6 or _lib.MATH_F32 for every convolution."""
         check(lib().sfa_model_set_math(self._h, int(math)), "sfa_model_set_math")
         self.math = int(math)
 
+    def set_side_streams(self, on: bool):
+        """Side stream for the level-0 heads on (default) or off (sfa_model_set_side_streams):
+        off when several forwards are kept in flight beside a copy stream, so the process's
+        streams fit HIP's 4 hardware queues. Not while a forward of this engine is running."""
+        with torch.cuda.device(self.device):
+            check(lib().sfa_model_set_side_streams(self._h, 1 if on else 0), "sfa_model_set_side_streams")
+        self.side_streams = bool(on)
+
     def twin(self) -> "KfpnEngine":
         """A second model handle over the SAME device weights (sfa_model_create does not copy
-        them): its own side stream and events, so two forwards can be in flight (or captured in
-        two graphs) on two streams. Workspaces are per engine / pipeline as usual."""
+        them): its own side stream and events (or none, like this engine), so two forwards can be
+        in flight (or captured in two graphs) on two streams. Workspaces are per engine /
+        pipeline as usual."""
         t = object.__new__(KfpnEngine)
         t.arch, t.device, t.heads, t.weights = self.arch, self.device, self.heads, self.weights
         h = ctypes.c_void_p()
@@ -95,7 +107,10 @@ class KfpnEngine:
                   "sfa_model_create")
         t._h = h
         t._ws = {}
+        t.side_streams = True
         t.set_math(self.math)
+        if not self.side_streams:
+            t.set_side_streams(False)
         return t
 
     def set_probe(self, flags: int):

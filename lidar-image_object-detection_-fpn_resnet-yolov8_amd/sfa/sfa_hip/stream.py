@@ -93,9 +93,11 @@ class StreamingDetector:
     ``inflight`` pipelines (each with its own buffers and model handle, ``KfpnEngine.twin``)
     take the batches in turn on their own streams; the forward + decode of each is a HIP graph
     (``graph=True``), the voxeliser (ragged per-batch frame offsets) is launched eagerly.
-    Default 1: with the copy stream beside them, two pipelines' streams (and their side
-    streams) exceed the 4 hardware queues per process and measured 7 % slower
-    (profiles/r02_stream_variants.txt).
+    Two pipelines need an engine without side streams (``KfpnEngine(..., side_streams=False)``;
+    the twins inherit it): with the copy stream beside them, two pipelines' streams AND their
+    side streams exceed HIP's 4 hardware queues per process and measured 7 % slower
+    (profiles/r02_stream_variants.txt); without side streams two pipelines are 13 % faster than
+    one (profiles/r02b_stream_side_streams.txt: 4,440 -> 5,010 frames/s). Default 1.
 
     ``run(callback)`` calls ``callback(dets_view, n_frames, batch_index)`` after each batch
     is enqueued, with that batch's stream current (dets are valid once that stream reaches

@@ -326,3 +326,25 @@ def test_head_probe_is_transparent(golden, gpu):
     for h in gc.HEADS:
         np.testing.assert_array_equal(base[h], probed[h], err_msg=f"{h}: probed forward differs")
         np.testing.assert_array_equal(base[h], after[h], err_msg=f"{h}: forward after the probe differs")
+
+
+def test_side_streams_off_on_bit_exact(golden, gpu):
+    """sfa_model_set_side_streams: the forward without side streams (every launch on the caller's
+    stream, as the multi-pipeline stream workload runs it), and again with them re-created, gives
+    the same bits as the default; twins inherit the setting."""
+    model = make_model(golden, gpu)
+    eng = model._engine(gpu)
+    eng.set_math(_math("fp16x3"))
+    x = torch.from_numpy(synthetic.synthetic_bev(3, 160, 192, seed=41)).to(gpu)
+    with torch.no_grad():
+        base = {h: v.cpu().numpy() for h, v in model(x).items()}
+        eng.set_side_streams(False)
+        try:
+            assert eng.twin().side_streams is False
+            off = {h: v.cpu().numpy() for h, v in model(x).items()}
+        finally:
+            eng.set_side_streams(True)
+        on = {h: v.cpu().numpy() for h, v in model(x).items()}
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(base[h], off[h], err_msg=f"{h}: forward without side streams differs")
+        np.testing.assert_array_equal(base[h], on[h], err_msg=f"{h}: forward after re-creating them differs")

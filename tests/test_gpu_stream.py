@@ -31,10 +31,12 @@ def test_device_stream_matches_fromfile(tmp_path, gpu):
         assert i == len(paths)
 
 
-@pytest.mark.parametrize("inflight,graph", [(1, True), (1, False), (2, True)])
-def test_streaming_detector_matches_pipeline(tmp_path, golden, gpu, inflight, graph):
+@pytest.mark.parametrize("inflight,graph,side", [(1, True, True), (1, False, True), (2, True, True),
+                                                 (2, True, False)])
+def test_streaming_detector_matches_pipeline(tmp_path, golden, gpu, inflight, graph, side):
     """Every configuration (forward + decode as a HIP graph or eager; 1 or 2 pipelines in flight,
-    the second on a twin model handle over the same weights) == the eager resident pipeline."""
+    the second on a twin model handle over the same weights; with or without the models' side
+    streams, as bench.py's stream workload runs 2 pipelines) == the eager resident pipeline."""
     clouds = [synthetic.synthetic_point_cloud(s) for s in range(1, 6)]  # 5 frames, batch 2
     paths = []
     for i, c in enumerate(clouds):
@@ -42,7 +44,8 @@ def test_streaming_detector_matches_pipeline(tmp_path, golden, gpu, inflight, gr
         c.tofile(p)
         paths.append(p)
     arch = _lib.make_arch(gc.HEADS)
-    eng = runtime.KfpnEngine(arch, runtime.pack_state_dict(gc.state_dict_np(golden.model), arch), gpu)
+    eng = runtime.KfpnEngine(arch, runtime.pack_state_dict(gc.state_dict_np(golden.model), arch), gpu,
+                             side_streams=side)
     got = []
     sd = StreamingDetector(eng, paths, batch=2, K=50, n_threads=2, inflight=inflight, graph=graph)
     sd.run(lambda dets, n, k: got.append(dets[:n].clone()))
