@@ -91,6 +91,15 @@ def parse():
     ap.add_argument("--stream-inflight", type=int, default=2,
                     help="--workload stream: pipelines in flight; with 2+ the engines run without "
                          "side streams (profiles/r02b_stream_side_streams.txt)")
+    ap.add_argument("--side-streams", choices=["auto", "on", "off"], default="auto",
+                    help="the models' level-0-heads side streams (sfa_model_set_side_streams); auto: "
+                         "on at N = 1, off at N > 1 (RCCL's stream then keeps a hardware queue)")
+    ap.add_argument("--gather-stream", choices=["step", "comm"], default="step",
+                    help="N > 1: the detections' all-gather on each step's own stream, or on one "
+                         "extra stream")
+    ap.add_argument("--sim-gather", action="store_true",
+                    help="N = 1: a device copy of the detections where the all-gather would go "
+                         "(rehearses the N > 1 stream layout on one GPU)")
     ap.add_argument("--share-weights", action="store_true",
                     help="the in-flight pipelines share one device copy of the packed weights "
                          "(KfpnEngine.twin) instead of one copy each")
@@ -473,29 +482,46 @@ def main():
     pipes = [build_pipeline(dev, args, rank)]
     for _ in range(nf - 1):  # own model handle each; weights shared (--share-weights) or a copy each
         pipes.append(build_pipeline(dev, args, rank, pipes[0].engine.twin() if args.share_weights else None))
+    # side streams: every stream of the process takes one of HIP's 4 hardware queues; with
+    # N > 1 RCCL adds its own stream, so the models run without theirs
+    # (profiles/r02b_ab_gather_streams.txt: the N > 1 layout rehearsed with --sim-gather).
+    side = {"on": True, "off": False, "auto": world == 1}[args.side_streams]
+    for p in pipes:
+        p.engine.set_side_streams(side)
     if args.serial_heads:
         for p in pipes:
             p.engine.set_probe(_lib.PROBE_SERIAL)
     steps = [StepGraphs(p, not args.no_graph) for p in pipes]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nf - 1)]
-    gather = world > 1
+    # --sim-gather (N = 1): a device copy of the detections in place of the all-gather, on the
+    # same stream the gather would use (the N > 1 stream layout rehearsed on one GPU)
+    gather = world > 1 or args.sim_gather
     if gather:
         import torch.distributed as dist
         from sfa_hip import dist as sdist
         frame_ids = torch.arange(rank * args.batch, (rank + 1) * args.batch, device=dev)
+        sim_out = torch.empty_like(pipes[0].dets)
 
-    if gather:
-        # all-gathers go on one stream in step order (the same collective order on every
+        def do_gather(dets):
+            if world > 1:
+                sdist.gather_detections(dets, frame_ids)
+            else:
+                sim_out.copy_(dets)
+
+    if gather and args.gather_stream == "comm":
+        # all-gathers on one extra stream in step order (the same collective order on every
         # rank); a pipeline's detections are overwritten only after their gather finished
         comm = torch.cuda.Stream()
         step_done = [torch.cuda.Event() for _ in range(nf)]
         comm_done = [torch.cuda.Event() for _ in range(nf)]
         gathered = [0] * nf
 
+    comm_mode = gather and args.gather_stream == "comm"
+
     def one_step(k, ev=None):
         i = k % nf
         with torch.cuda.stream(streams[i]):
-            if gather and gathered[i]:
+            if comm_mode and gathered[i]:
                 streams[i].wait_event(comm_done[i])
             if ev is not None:
                 ev[0].record()
@@ -505,12 +531,16 @@ def main():
             steps[i].run(1)
             if ev is not None:
                 ev[2].record()
-            if gather:
+            if comm_mode:
                 step_done[i].record()
-        if gather:
+            elif gather:
+                # on the step's own stream, in step order (the same collective order on every
+                # rank); RCCL's stream waits for this step only, the other pipeline runs on
+                do_gather(pipes[i].dets)
+        if comm_mode:
             with torch.cuda.stream(comm):
                 comm.wait_event(step_done[i])
-                sdist.gather_detections(pipes[i].dets, frame_ids)
+                do_gather(pipes[i].dets)
                 comm_done[i].record()
             gathered[i] = 1
 
@@ -585,6 +615,7 @@ def main():
                 "parallelism": f"dp{world} (frame-sharded replicas; RCCL all_gather of detections)",
                 "hip_graph": not args.no_graph,
                 "steps_in_flight": nf,
+                "side_streams": side,
             },
             "stages_ms": {"forward": round(fwd_ms, 4), "decode": round(dec_ms, 4),
                           "note": "one step in flight; value/ms_per_step use %d in flight" % nf},
