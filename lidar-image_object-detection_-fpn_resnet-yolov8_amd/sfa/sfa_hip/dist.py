@@ -3,8 +3,8 @@
 Frames are independent (fpn_resnet.py:169-246, evaluation_utils.py:77-105), so a
 KITTI stream is split into batches of ``batch`` consecutive frames and batch j is
 owned by rank j % world.  Each rank voxelises, infers and decodes its own frames;
-the only collective is one RCCL (backend "nccl" on ROCm) all-gather of the fixed
-shape (B, K, 10) detections plus their frame ids per step.
+the only collective is one RCCL (backend "nccl" on ROCm) all-gather per step of the fixed
+shape (B, K, 10) detections with their frame ids packed into the same rows.
 """
 
 from __future__ import annotations
@@ -29,25 +29,29 @@ def steps_per_rank(num_frames: int, batch: int, world: int) -> int:
 
 
 def gather_detections(dets: torch.Tensor, frame_ids: torch.Tensor, group=None):
-    """All-gather (B, K, 10) detections and (B,) int64 frame ids (-1 = padding).
+    """All-gather (B, K, 10) float32 detections and (B,) int64 frame ids (-1 = padding) as ONE
+    collective: each frame's row is its K*10 floats followed by its id's 8 bytes (bit-cast,
+    so every id survives exactly), B * (K*10 + 2) * 4 bytes per rank.
 
     Returns (world*B, K, 10) and (world*B,) on every rank, rank-major."""
     world = dist.get_world_size(group)
     if world == 1:
         return dets, frame_ids
+    if dets.dtype != torch.float32 or frame_ids.dtype != torch.int64:
+        raise TypeError("gather_detections: float32 detections and int64 frame ids")
     B = dets.shape[0]
-    out = torch.empty((world * B,) + tuple(dets.shape[1:]), dtype=dets.dtype, device=dets.device)
-    ids = torch.empty((world * B,), dtype=frame_ids.dtype, device=frame_ids.device)
+    row = dets[0].numel()
+    packed = torch.cat([dets.reshape(B, row), frame_ids.contiguous().view(torch.float32).view(B, 2)], 1)
+    out = torch.empty((world * B, row + 2), dtype=torch.float32, device=dets.device)
     if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, dets.contiguous(), group=group)
-        dist.all_gather_into_tensor(ids, frame_ids.contiguous(), group=group)
+        dist.all_gather_into_tensor(out, packed, group=group)
     else:  # gloo (CPU tests / single-GPU rehearsal): gather through host memory
-        oc, ic = out.cpu(), ids.cpu()
-        dist.all_gather(list(oc.chunk(world)), dets.contiguous().cpu(), group=group)
-        dist.all_gather(list(ic.chunk(world)), frame_ids.contiguous().cpu(), group=group)
+        oc = out.cpu()
+        dist.all_gather(list(oc.chunk(world)), packed.cpu(), group=group)
         out.copy_(oc)
-        ids.copy_(ic)
-    return out, ids
+    d = out[:, :row].reshape((world * B,) + tuple(dets.shape[1:]))
+    ids = out[:, row:].contiguous().view(torch.int64).reshape(world * B)
+    return d, ids
 
 
 def order_by_frame(dets: torch.Tensor, ids: torch.Tensor):

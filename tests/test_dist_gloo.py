@@ -68,3 +68,36 @@ def test_shard_batches_partition():
                               for r in range(w)])
         np.testing.assert_array_equal(np.sort(got), np.arange(n))
         assert max(len(sdist.shard_batches(n, b, w, r)) for r in range(w)) == sdist.steps_per_rank(n, b, w)
+
+
+def _worker_big_ids(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        dets = torch.full((3, 4, 10), float(rank))
+        ids = torch.tensor([2 ** 40 + rank, -1, 2 ** 24 + 1 + rank], dtype=torch.int64)
+        d, i = sdist.gather_detections(dets, ids)
+        q.put((rank, d.numpy(), i.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_packs_ids_exactly():
+    """The one-collective gather bit-casts the int64 frame ids into the detection rows: ids beyond
+    float32's integer range and the -1 padding marker come back exactly."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_big_ids, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for _, d, i in res:
+        np.testing.assert_array_equal(i, [2 ** 40, -1, 2 ** 24 + 1, 2 ** 40 + 1, -1, 2 ** 24 + 2])
+        assert d.shape == (6, 4, 10)
+        np.testing.assert_array_equal(d[:3], 0.0)
+        np.testing.assert_array_equal(d[3:], 1.0)
