@@ -359,12 +359,21 @@ def run_stream(args, rank, world, dev):
         warm.close()
         det = StreamingDetector(engine, [files[i % len(files)] for i in range(args.batch * args.steps)],
                                 args.batch, args.K, threads, inflight=args.stream_inflight, graph=not args.no_graph)
+        gather_cb = None
         if world > 1:
             import torch.distributed as dist
+            from sfa_hip import dist as sdist
+            slot = torch.arange(args.batch, device=dev)
+
+            def gather_cb(dets, n, k):
+                # configs[3]: each batch's decoded boxes all-gathered on the batch's own stream
+                # (global frame ids; -1 marks the slots of a short last batch)
+                ids = torch.where(slot < n, (k * world + rank) * args.batch + slot, torch.full_like(slot, -1))
+                sdist.gather_detections(dets, ids)
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        det.run()
+        det.run(gather_cb)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -456,7 +465,9 @@ def main():
                 data = "synthetic 132,880-pt sweeps written as KITTI .bin files (page cache)"
                 cfg = {"workload": "KITTI .bin stream -> pinned DMA -> BEV -> fpn_resnet_18 "
                                    "forward -> decode K=%d, bs=%d per GPU (forward + decode as a "
-                                   "HIP graph, BEV eager: per-batch frame offsets)" % (args.K, args.batch),
+                                   "HIP graph, BEV eager: per-batch frame offsets)%s"
+                                   % (args.K, args.batch, " -> all-gather of each batch's detections"
+                                      if world > 1 else ""),
                        "reader_threads": threads, "global_batch": world * args.batch,
                        "steps_in_flight": max(1, args.stream_inflight)}
             else:
