@@ -267,6 +267,40 @@ def probe_heads(args, pipe, step):
     return np.median(np.array(per), axis=0).tolist()  # ms per level
 
 
+def probe_bev(args, pipe, reps=20):
+    """configs[2]: the BEV voxelisation pass alone (filter fused, scatter + gather kernels of
+    sfa_bev_voxelize) on the pipeline's resident sweeps, HIP events on the launching stream,
+    against the HBM roofline: algorithmic bytes = N * 16 (xyzi read) + 3 * 608^2 * 4 (f32 map
+    written) per frame; scratch key / count traffic is not algorithmic."""
+    if args.workload != "e2e":
+        return None
+    st = _lib.stream_ptr(pipe.dev)
+
+    def vox():
+        pipe.vox(pipe.points, pipe.offsets, layout=_lib.BEV_NHWC4_F32, flags=_lib.BEV_RAW, out=pipe.bev,
+                 stream=st)
+
+    vox()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        vox()
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    npts = int(pipe.offsets[-1])
+    algo = npts * 16 + pipe.B * 3 * 608 * 608 * 4
+    ach = algo / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "unit": "GB/s", "achieved": round(ach, 1), "peak": 8000.0,
+            "frac": round(ach / 8000.0, 4), "traffic": None,
+            "kernel": "sfa_bev_voxelize (SFA_BEV_RAW: filter fused; bev_scatter_kernel + bev_gather_kernel)",
+            "us_per_batch": round(1e3 * ms, 1), "points_per_batch": npts,
+            "algorithmic_bytes_per_batch": algo,
+            "measured": "HIP events around %d back-to-back voxelisations of the step's %d sweeps, "
+                        "one stream, nothing else running" % (reps, pipe.B)}
+
+
 def roofline_line(args, heads, forward_roofline, fwd_achieved, peak, peak_basis, capped):
     line = {"bound": "mfma", "unit": "TFLOP/s", "peak": round(peak, 2), "peak_basis": peak_basis,
             "peak_power_capped": round(capped, 2) if capped else None,
@@ -579,6 +613,7 @@ def main():
     fwd_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in ev]))
     dec_ms = float(np.mean([e[1].elapsed_time(e[2]) for e in ev]))
     heads = probe_heads(args, pipes[0], steps[0]) if rank == 0 and args.probe_forwards > 0 else None
+    bev_roof = probe_bev(args, pipes[0]) if rank == 0 else None
     if world > 1:
         t = torch.tensor([elapsed, fwd_ms, dec_ms], dtype=torch.float64,
                          device=dev if dist.get_backend() == "nccl" else "cpu")
@@ -632,6 +667,8 @@ def main():
                           "note": "one step in flight; value/ms_per_step use %d in flight" % nf},
             "roofline": roofline_line(args, heads, forward_roofline, achieved, peak, peak_basis, capped),
         }
+        if bev_roof is not None:
+            line["bev_roofline"] = bev_roof
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(line), flush=True)
