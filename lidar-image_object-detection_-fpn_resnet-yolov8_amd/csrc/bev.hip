@@ -14,6 +14,9 @@
 //     density = min(1, ln(count+1)/ln 64) (f64 table), written in the requested
 //     layout; the scratch cell is re-zeroed for the next call.
 // The result is independent of atomic arrival order: bit-exact.
+#include <cstdlib>
+#include <cstring>
+
 #include "common.h"
 
 namespace sfa {
@@ -31,6 +34,35 @@ struct BevArgs {
   double density[64];  // min(1, ln(c+1)/ln 64), c = 0..63 (c >= 63 -> 1)
 };
 
+// The cell and the 64-bit top-point key of point i of a frame (false: the point is dropped).
+template <bool RAW>
+__device__ __forceinline__ bool bev_point_cell(const float4 p, const BevArgs& a, int64_t i, int& cell,
+                                               unsigned long long& key) {
+  float zr = p.z;
+  if (RAW) {
+    // kitti_data_utils.py:237-239 — inclusive on both ends, NaN fails.
+    if (!(p.x >= a.minX && p.x <= a.maxX && p.y >= a.minY && p.y <= a.maxY && p.z >= a.minZ &&
+          p.z <= a.maxZ))
+      return false;
+    zr = __fsub_rn(p.z, a.minZ);  // :241
+  } else if (!(zr >= 0.f)) {
+    // makeBEVMap on already-filtered points: z is >= 0 after the filter; a negative or
+    // NaN z has no defined top-point order (the 64-bit key needs z >= +0) -> skipped.
+    return false;
+  }
+  int row = (int)floorf(__fdiv_rn(p.x, a.disc));                      // kitti_bev_utils.py:28
+  int col = (int)__fadd_rn(floorf(__fdiv_rn(p.y, a.disc)), a.half_w);  // :29 (np.int_ truncates)
+  // numpy fancy indexing wraps negative indices of the (609, 609) maps (:44-48).
+  if (row < 0) row += kBevH + 1;
+  if (col < 0) col += kBevW + 1;
+  // :50-53 crop to [:608, :608]; indices outside the (609, 609) table (IndexError in
+  // numpy) cannot occur after the filter and are skipped for pre-filtered input.
+  if (row < 0 || row >= kBevH || col < 0 || col >= kBevW) return false;
+  cell = row * kBevW + col;
+  key = ((unsigned long long)__float_as_uint(zr) << 32) | (unsigned)(~(unsigned)i);
+  return true;
+}
+
 template <bool RAW>
 __global__ void __launch_bounds__(256) bev_scatter_kernel(const float4* __restrict__ pts,
                                                           BevArgs a,
@@ -41,56 +73,26 @@ __global__ void __launch_bounds__(256) bev_scatter_kernel(const float4* __restri
   const int64_t n = a.start[b + 1] - s;
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const float4 p = pts[s + i];
-  float zr = p.z;
-  if (RAW) {
-    // kitti_data_utils.py:237-239 — inclusive on both ends, NaN fails.
-    if (!(p.x >= a.minX && p.x <= a.maxX && p.y >= a.minY && p.y <= a.maxY && p.z >= a.minZ &&
-          p.z <= a.maxZ))
-      return;
-    zr = __fsub_rn(p.z, a.minZ);  // :241
-  } else if (!(zr >= 0.f)) {
-    // makeBEVMap on already-filtered points: z is >= 0 after the filter; a negative or
-    // NaN z has no defined top-point order (the 64-bit key needs z >= +0) -> skipped.
-    return;
-  }
-  int row = (int)floorf(__fdiv_rn(p.x, a.disc));                      // kitti_bev_utils.py:28
-  int col = (int)__fadd_rn(floorf(__fdiv_rn(p.y, a.disc)), a.half_w);  // :29 (np.int_ truncates)
-  // numpy fancy indexing wraps negative indices of the (609, 609) maps (:44-48).
-  if (row < 0) row += kBevH + 1;
-  if (col < 0) col += kBevW + 1;
-  // :50-53 crop to [:608, :608]; indices outside the (609, 609) table (IndexError in
-  // numpy) cannot occur after the filter and are skipped for pre-filtered input.
-  if (row < 0 || row >= kBevH || col < 0 || col >= kBevW) return;
-  const int cell = row * kBevW + col;
-  const unsigned long long key =
-      ((unsigned long long)__float_as_uint(zr) << 32) | (unsigned)(~(unsigned)i);
-  unsigned long long* kp = keys + (size_t)b * kBevCells + cell;
-  atomicMax(kp, key);
+  int cell;
+  unsigned long long key;
+  if (!bev_point_cell<RAW>(pts[s + i], a, i, cell, key)) return;
+  atomicMax(keys + (size_t)b * kBevCells + cell, key);
   atomicAdd(counts + (size_t)b * kBevCells + cell, 1u);
 }
 
+// One output cell: intensity = i[top], height = z'/4.0 (f32), density from the count (f64
+// table), stored in the requested layout (torch.flip(bev, [1, 2]) when FLIP).
 template <int LAYOUT, bool FLIP>
-__global__ void __launch_bounds__(256) bev_gather_kernel(const float4* __restrict__ pts, BevArgs a,
-                                                         unsigned long long* __restrict__ keys,
-                                                         unsigned* __restrict__ counts,
-                                                         void* __restrict__ out) {
-  const int b = blockIdx.y;
-  const int cell = blockIdx.x * blockDim.x + threadIdx.x;
-  if (cell >= kBevCells) return;
-  const size_t sc = (size_t)b * kBevCells + cell;
-  const unsigned cnt = counts[sc];
+__device__ __forceinline__ void bev_store_cell(const float4* __restrict__ pts, const BevArgs& a, int b, int cell,
+                                               unsigned cnt, unsigned long long key, void* __restrict__ out) {
   float inten = 0.f, height = 0.f;
   double dens = 0.0;
   if (cnt) {
-    const unsigned long long key = keys[sc];
     const unsigned idx = ~(unsigned)(key & 0xffffffffull);
     const float zr = __uint_as_float((unsigned)(key >> 32));
     inten = pts[a.start[b] + idx].w;
     height = __fdiv_rn(zr, a.max_height);  // :43-44, f32 division
     dens = a.density[cnt < 63u ? cnt : 63u];
-    keys[sc] = 0ull;  // leave scratch zeroed for the next call
-    counts[sc] = 0u;
   }
   // torch.flip(bev, [1, 2]): cell (r, c) lands at (607 - r, 607 - c)
   const int oc = FLIP ? kBevCells - 1 - cell : cell;
@@ -108,6 +110,168 @@ __global__ void __launch_bounds__(256) bev_gather_kernel(const float4* __restric
     o[kBevCells] = (double)height;
     o[2 * kBevCells] = dens;
   }
+}
+
+template <int LAYOUT, bool FLIP>
+__global__ void __launch_bounds__(256) bev_gather_kernel(const float4* __restrict__ pts, BevArgs a,
+                                                         unsigned long long* __restrict__ keys,
+                                                         unsigned* __restrict__ counts,
+                                                         void* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int cell = blockIdx.x * blockDim.x + threadIdx.x;
+  if (cell >= kBevCells) return;
+  const size_t sc = (size_t)b * kBevCells + cell;
+  const unsigned cnt = counts[sc];
+  unsigned long long key = 0ull;
+  if (cnt) {
+    key = keys[sc];
+    keys[sc] = 0ull;  // leave scratch zeroed for the next call
+    counts[sc] = 0u;
+  }
+  bev_store_cell<LAYOUT, FLIP>(pts, a, b, cell, cnt, key, out);
+}
+
+// ------------------------------------------------------------ binned path --
+// The default when the batch's points fit the scratch as records (any KITTI-sized sweep).
+// The atomic path above does two device-scope atomics per kept point on a 12-B-per-cell
+// scratch spread over the whole map: each is an L2 miss on its own line (the scatter was
+// 58 us for 16 sweeps, the gather 38 us). Here the points are binned by 8-row strips of
+// the map (76 per frame) and each strip is reduced in LDS:
+//   count   per point: its strip; LDS histogram per block, one global add per strip
+//   scan    strip offsets in (frame, strip) order (one small block)
+//   bin     per point again: a slot in its strip's range (LDS-aggregated reservations),
+//           record = {key (8 B), cell within the strip, 0}
+//   strip   per (frame, strip): ds_max_u64 / ds_add_u32 over its records in LDS (4,864
+//           cells: 58 KiB), then every cell of the strip written in the output layout.
+// The same keys and counts reach every cell (max and + are order-free): bit-identical to the
+// atomic path. Self-cleaning like it: the strip pass zeroes the records it read and its
+// strip's counters, so the scratch is zero again when the call's kernels have run.
+constexpr int kStripRows = 8;
+constexpr int kStripCells = kStripRows * kBevW;   // 4,864
+constexpr int kStrips = kBevH / kStripRows;       // 76
+constexpr int kStripThreads = 512;
+
+struct BinScratch {
+  unsigned* count;   // [B][kStrips] points per strip
+  unsigned* offset;  // [B][kStrips] first record of the strip
+  unsigned* cursor;  // [B][kStrips] next free record (reservation counter)
+  uint4* rec;        // records
+};
+
+template <bool RAW>
+__global__ void __launch_bounds__(256) bev_bin_count_kernel(const float4* __restrict__ pts, BevArgs a,
+                                                            BinScratch bs) {
+  __shared__ unsigned hist[kStrips];
+  const int b = blockIdx.y;
+  const int64_t s = a.start[b];
+  const int64_t n = a.start[b + 1] - s;
+  for (int t = threadIdx.x; t < kStrips; t += blockDim.x) hist[t] = 0u;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int cell;
+  unsigned long long key;
+  if (i < n && bev_point_cell<RAW>(pts[s + i], a, i, cell, key)) atomicAdd(&hist[cell / kStripCells], 1u);
+  __syncthreads();
+  for (int t = threadIdx.x; t < kStrips; t += blockDim.x)
+    if (hist[t]) atomicAdd(&bs.count[b * kStrips + t], hist[t]);
+}
+
+// one block: the exclusive scan of the (frame, strip) counts in that order -> record offsets
+// (thread t owns up to kScanPer consecutive bins; wave-level then block-level scan)
+constexpr int kScanThreads = 1024;
+constexpr int kScanPer = (SFA_BEV_MAX_BATCH * kStrips + kScanThreads - 1) / kScanThreads;
+__global__ void __launch_bounds__(kScanThreads) bev_bin_scan_kernel(BinScratch bs, int batch) {
+  __shared__ unsigned wsum[kScanThreads / 64];
+  const int nbin = batch * kStrips, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  unsigned v[kScanPer], sum = 0;
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) {
+    const int i = t * kScanPer + j;
+    v[j] = i < nbin ? bs.count[i] : 0u;
+    sum += v[j];
+  }
+  unsigned inc = sum;  // inclusive scan of the thread sums within the wave
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned o = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  if (w == 0) {
+    unsigned x = lane < kScanThreads / 64 ? wsum[lane] : 0u, xi = x;
+#pragma unroll
+    for (int d = 1; d < kScanThreads / 64; d <<= 1) {
+      const unsigned o = __shfl_up(xi, d, 64);
+      if (lane >= d) xi += o;
+    }
+    if (lane < kScanThreads / 64) wsum[lane] = xi - x;  // exclusive wave offsets
+  }
+  __syncthreads();
+  unsigned run = wsum[w] + inc - sum;
+#pragma unroll
+  for (int j = 0; j < kScanPer; ++j) {
+    const int i = t * kScanPer + j;
+    if (i < nbin) {
+      bs.offset[i] = run;
+      bs.cursor[i] = run;
+    }
+    run += v[j];
+  }
+}
+
+template <bool RAW>
+__global__ void __launch_bounds__(256) bev_bin_kernel(const float4* __restrict__ pts, BevArgs a, BinScratch bs) {
+  __shared__ unsigned hist[kStrips], base[kStrips];
+  const int b = blockIdx.y;
+  const int64_t s = a.start[b];
+  const int64_t n = a.start[b + 1] - s;
+  for (int t = threadIdx.x; t < kStrips; t += blockDim.x) hist[t] = 0u;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int cell = 0, strip = 0;
+  unsigned long long key = 0ull;
+  unsigned slot = 0;
+  const bool ok = i < n && bev_point_cell<RAW>(pts[s + i], a, i, cell, key);
+  if (ok) {
+    strip = cell / kStripCells;
+    slot = atomicAdd(&hist[strip], 1u);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < kStrips; t += blockDim.x)
+    base[t] = hist[t] ? atomicAdd(&bs.cursor[b * kStrips + t], hist[t]) : 0u;
+  __syncthreads();
+  if (ok)
+    bs.rec[base[strip] + slot] =
+        make_uint4((unsigned)(key & 0xffffffffull), (unsigned)(key >> 32), (unsigned)(cell - strip * kStripCells), 0u);
+}
+
+template <int LAYOUT, bool FLIP>
+__global__ void __launch_bounds__(kStripThreads) bev_strip_kernel(const float4* __restrict__ pts, BevArgs a,
+                                                                  BinScratch bs, void* __restrict__ out) {
+  __shared__ unsigned long long skey[kStripCells];
+  __shared__ unsigned scnt[kStripCells];
+  const int strip = blockIdx.x, b = blockIdx.y, bin = b * kStrips + strip;
+  for (int c = threadIdx.x; c < kStripCells; c += kStripThreads) {
+    skey[c] = 0ull;
+    scnt[c] = 0u;
+  }
+  __syncthreads();
+  const unsigned off = bs.offset[bin], cnt = bs.count[bin];
+  for (unsigned r = threadIdx.x; r < cnt; r += kStripThreads) {
+    const uint4 rec = bs.rec[off + r];
+    bs.rec[off + r] = make_uint4(0u, 0u, 0u, 0u);  // scratch zero again for the next call
+    atomicMax(&skey[rec.z], ((unsigned long long)rec.y << 32) | rec.x);
+    atomicAdd(&scnt[rec.z], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    bs.count[bin] = 0u;
+    bs.offset[bin] = 0u;
+    bs.cursor[bin] = 0u;
+  }
+  for (int c = threadIdx.x; c < kStripCells; c += kStripThreads)
+    bev_store_cell<LAYOUT, FLIP>(pts, a, b, strip * kStripCells + c, scnt[c], skey[c], out);
 }
 
 }  // namespace sfa
@@ -163,6 +327,52 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
       reinterpret_cast<char*>(scratch) +
       align_up((size_t)batch * kBevCells * sizeof(unsigned long long), 256));
   const float4* p4 = reinterpret_cast<const float4*>(points);
+  // binned path (default) when the batch's points fit the scratch as 16-B records
+  const size_t bin_bytes = align_up((size_t)batch * kStrips * sizeof(unsigned), 256);
+  const size_t scratch_bytes = sfa_bev_scratch_size(batch);
+  const int64_t total = frame_offsets[batch] - frame_offsets[0];
+  const char* fa = getenv("SFA_BEV_ATOMIC");  // the atomic path (A/B, the equivalence test)
+  const bool force_atomic = fa && strcmp(fa, "0") != 0;
+  if (!force_atomic && 3 * bin_bytes < scratch_bytes &&
+      (uint64_t)total <= (uint64_t)((scratch_bytes - 3 * bin_bytes) / sizeof(uint4)) && total < (int64_t)0xffffffff) {
+    char* sb = reinterpret_cast<char*>(scratch);
+    BinScratch bs;
+    bs.count = reinterpret_cast<unsigned*>(sb);
+    bs.offset = reinterpret_cast<unsigned*>(sb + bin_bytes);
+    bs.cursor = reinterpret_cast<unsigned*>(sb + 2 * bin_bytes);
+    bs.rec = reinterpret_cast<uint4*>(sb + 3 * bin_bytes);
+    if (max_n > 0) {
+      dim3 g1((unsigned)((max_n + 255) / 256), batch);
+      if (flags == SFA_BEV_RAW)
+        hipLaunchKernelGGL(bev_bin_count_kernel<true>, g1, dim3(256), 0, st, p4, a, bs);
+      else
+        hipLaunchKernelGGL(bev_bin_count_kernel<false>, g1, dim3(256), 0, st, p4, a, bs);
+      SFA_LAUNCH_CHECK();
+      hipLaunchKernelGGL(bev_bin_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, bs, batch);
+      SFA_LAUNCH_CHECK();
+      if (flags == SFA_BEV_RAW)
+        hipLaunchKernelGGL(bev_bin_kernel<true>, g1, dim3(256), 0, st, p4, a, bs);
+      else
+        hipLaunchKernelGGL(bev_bin_kernel<false>, g1, dim3(256), 0, st, p4, a, bs);
+      SFA_LAUNCH_CHECK();
+    }
+    dim3 g3(kStrips, batch);
+#define SFA_BEV_STRIP(L, F) \
+  hipLaunchKernelGGL((bev_strip_kernel<L, F>), g3, dim3(kStripThreads), 0, st, p4, a, bs, out)
+    switch (out_layout) {
+      case SFA_BEV_NCHW3_F32:
+        if (flip) SFA_BEV_STRIP(SFA_BEV_NCHW3_F32, true); else SFA_BEV_STRIP(SFA_BEV_NCHW3_F32, false);
+        break;
+      case SFA_BEV_NCHW3_F64:
+        if (flip) SFA_BEV_STRIP(SFA_BEV_NCHW3_F64, true); else SFA_BEV_STRIP(SFA_BEV_NCHW3_F64, false);
+        break;
+      default:
+        if (flip) SFA_BEV_STRIP(SFA_BEV_NHWC4_F32, true); else SFA_BEV_STRIP(SFA_BEV_NHWC4_F32, false);
+    }
+#undef SFA_BEV_STRIP
+    SFA_LAUNCH_CHECK();
+    return SFA_OK;
+  }
   if (max_n > 0) {
     dim3 g1((unsigned)((max_n + 255) / 256), batch);
     if (flags == SFA_BEV_RAW)

@@ -103,3 +103,55 @@ def test_filter_large_random(gpu):
 def test_cpu_input_refused():
     with pytest.raises(_lib.SfaNativeError):
         runtime.filter_points(torch.zeros(4, 4), gc.BOUNDARY)
+
+
+@pytest.mark.parametrize("flip", [False, True])
+def test_binned_path_equals_atomic_path(gpu, monkeypatch, flip):
+    """The default binned voxeliser (points binned by 8-row strips, each strip reduced in LDS)
+    gives the bits of the global-atomic one (SFA_BEV_ATOMIC=1) in every layout, flipped or not,
+    on a ragged batch with a saturated-density cell and an empty frame; both leave the scratch
+    zeroed."""
+    from sfa_hip import synthetic
+    rng = np.random.default_rng(11)
+    dense = np.zeros((5000, 4), np.float32)  # one cell, > 63 points (density cap), z ties
+    dense[:, 0] = 20.01
+    dense[:, 1] = 0.01
+    dense[:, 2] = rng.choice(np.float32([-1.5, 0.25, 0.25]), 5000)
+    dense[:, 3] = rng.uniform(0, 1, 5000)
+    clouds = [synthetic.synthetic_point_cloud(s) for s in (7, 8)] + [dense, np.zeros((0, 4), np.float32),
+                                                                      synthetic.synthetic_point_cloud(9)]
+    offs = np.cumsum([0] + [c.shape[0] for c in clouds])
+    pts = torch.from_numpy(np.concatenate(clouds)).to(gpu)
+    vox = runtime.BevVoxelizer(gpu, len(clouds))
+    flags = _lib.BEV_RAW | (_lib.BEV_FLIP_HW if flip else 0)
+    for layout in (_lib.BEV_NCHW3_F64, _lib.BEV_NCHW3_F32, _lib.BEV_NHWC4_F32):
+        monkeypatch.delenv("SFA_BEV_ATOMIC", raising=False)
+        binned = vox(pts, offs, gc.BOUNDARY, layout=layout, flags=flags).cpu().numpy()
+        assert int(vox.scratch.count_nonzero()) == 0
+        monkeypatch.setenv("SFA_BEV_ATOMIC", "1")
+        atomic = vox(pts, offs, gc.BOUNDARY, layout=layout, flags=flags).cpu().numpy()
+        assert int(vox.scratch.count_nonzero()) == 0
+        np.testing.assert_array_equal(binned, atomic)
+    monkeypatch.delenv("SFA_BEV_ATOMIC", raising=False)
+    f64 = vox(pts, offs, gc.BOUNDARY, layout=_lib.BEV_NCHW3_F64).cpu().numpy()
+    for i, c in enumerate(clouds):
+        exp = bev_oracle.makeBEVMap(bev_oracle.get_filtered_lidar(c, gc.BOUNDARY), gc.BOUNDARY)
+        np.testing.assert_array_equal(f64[i], exp)
+
+
+def test_oversized_frame_uses_atomic_path(gpu):
+    """A batch with more points than the scratch holds as records (here 1 frame of 400,000 points,
+    capacity ~277 k) takes the global-atomic path: still bit-exact, scratch still clean."""
+    rng = np.random.default_rng(13)
+    n = 400_000
+    pts = np.zeros((n, 4), np.float32)
+    pts[:, 0] = rng.uniform(-1, 51, n)
+    pts[:, 1] = rng.uniform(-26, 26, n)
+    pts[:, 2] = rng.uniform(-3, 1.5, n)
+    pts[:, 3] = rng.uniform(0, 1, n)
+    vox = runtime.BevVoxelizer(gpu, 1)
+    assert n * 16 > vox.scratch.numel()
+    got = vox(torch.from_numpy(pts).to(gpu), [0, n], gc.BOUNDARY, layout=_lib.BEV_NCHW3_F64).cpu().numpy()[0]
+    assert int(vox.scratch.count_nonzero()) == 0
+    exp = bev_oracle.makeBEVMap(bev_oracle.get_filtered_lidar(pts, gc.BOUNDARY), gc.BOUNDARY)
+    np.testing.assert_array_equal(got, exp)
