@@ -158,6 +158,8 @@ struct BinScratch {
   uint4* rec;        // records
 };
 
+constexpr int kBinPPT = 4;  // points per thread of the count / bin passes (strided by the block)
+
 template <bool RAW>
 __global__ void __launch_bounds__(256) bev_bin_count_kernel(const float4* __restrict__ pts, BevArgs a,
                                                             BinScratch bs) {
@@ -167,10 +169,13 @@ __global__ void __launch_bounds__(256) bev_bin_count_kernel(const float4* __rest
   const int64_t n = a.start[b + 1] - s;
   for (int t = threadIdx.x; t < kStrips; t += blockDim.x) hist[t] = 0u;
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int cell;
-  unsigned long long key;
-  if (i < n && bev_point_cell<RAW>(pts[s + i], a, i, cell, key)) atomicAdd(&hist[cell / kStripCells], 1u);
+#pragma unroll
+  for (int j = 0; j < kBinPPT; ++j) {
+    const int64_t i = ((int64_t)blockIdx.x * kBinPPT + j) * blockDim.x + threadIdx.x;
+    int cell;
+    unsigned long long key;
+    if (i < n && bev_point_cell<RAW>(pts[s + i], a, i, cell, key)) atomicAdd(&hist[cell / kStripCells], 1u);
+  }
   __syncthreads();
   for (int t = threadIdx.x; t < kStrips; t += blockDim.x)
     if (hist[t]) atomicAdd(&bs.count[b * kStrips + t], hist[t]);
@@ -228,22 +233,26 @@ __global__ void __launch_bounds__(256) bev_bin_kernel(const float4* __restrict__
   const int64_t n = a.start[b + 1] - s;
   for (int t = threadIdx.x; t < kStrips; t += blockDim.x) hist[t] = 0u;
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int cell = 0, strip = 0;
-  unsigned long long key = 0ull;
-  unsigned slot = 0;
-  const bool ok = i < n && bev_point_cell<RAW>(pts[s + i], a, i, cell, key);
-  if (ok) {
-    strip = cell / kStripCells;
-    slot = atomicAdd(&hist[strip], 1u);
+  int cell[kBinPPT], strip[kBinPPT];
+  unsigned long long key[kBinPPT];
+  unsigned slot[kBinPPT];
+  bool ok[kBinPPT];
+#pragma unroll
+  for (int j = 0; j < kBinPPT; ++j) {
+    const int64_t i = ((int64_t)blockIdx.x * kBinPPT + j) * blockDim.x + threadIdx.x;
+    ok[j] = i < n && bev_point_cell<RAW>(pts[s + i], a, i, cell[j], key[j]);
+    strip[j] = ok[j] ? cell[j] / kStripCells : 0;
+    slot[j] = ok[j] ? atomicAdd(&hist[strip[j]], 1u) : 0u;
   }
   __syncthreads();
   for (int t = threadIdx.x; t < kStrips; t += blockDim.x)
     base[t] = hist[t] ? atomicAdd(&bs.cursor[b * kStrips + t], hist[t]) : 0u;
   __syncthreads();
-  if (ok)
-    bs.rec[base[strip] + slot] =
-        make_uint4((unsigned)(key & 0xffffffffull), (unsigned)(key >> 32), (unsigned)(cell - strip * kStripCells), 0u);
+#pragma unroll
+  for (int j = 0; j < kBinPPT; ++j)
+    if (ok[j])
+      bs.rec[base[strip[j]] + slot[j]] = make_uint4((unsigned)(key[j] & 0xffffffffull), (unsigned)(key[j] >> 32),
+                                                    (unsigned)(cell[j] - strip[j] * kStripCells), 0u);
 }
 
 template <int LAYOUT, bool FLIP>
@@ -342,7 +351,7 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
     bs.cursor = reinterpret_cast<unsigned*>(sb + 2 * bin_bytes);
     bs.rec = reinterpret_cast<uint4*>(sb + 3 * bin_bytes);
     if (max_n > 0) {
-      dim3 g1((unsigned)((max_n + 255) / 256), batch);
+      dim3 g1((unsigned)((max_n + 256 * kBinPPT - 1) / (256 * kBinPPT)), batch);
       if (flags == SFA_BEV_RAW)
         hipLaunchKernelGGL(bev_bin_count_kernel<true>, g1, dim3(256), 0, st, p4, a, bs);
       else
