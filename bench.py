@@ -82,9 +82,10 @@ def parse():
                          "of synthetic 132,880-point sweeps (sparse like KITTI; made on the GPU before "
                          "the timed region)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=None,
                     help="steps in flight on separate streams (each with its own buffers and "
-                         "model handle); >1 lets one step's kernel tails overlap the next's")
+                         "model handle); >1 lets one step's kernel tails overlap the next's. "
+                         "Default 2; 3 for --workload fusion (bs=8: profiles/r02c_ab_fusion_inflight3.txt)")
     ap.add_argument("--fusion-nms", choices=["greedy", "gaussian"], default="greedy",
                     help="--workload fusion: test6.py's greedy NMS or the README's Gaussian soft-NMS "
                          "(README.md:250-261)")
@@ -93,7 +94,7 @@ def parse():
                          "side streams (profiles/r02b_stream_side_streams.txt)")
     ap.add_argument("--side-streams", choices=["auto", "on", "off"], default="auto",
                     help="the models' level-0-heads side streams (sfa_model_set_side_streams); auto: "
-                         "on at N = 1, off at N > 1 (RCCL's stream then keeps a hardware queue)")
+                         "on at N = 1 with at most 2 steps in flight, else off (side_streams_for)")
     ap.add_argument("--gather-stream", choices=["step", "comm"], default="step",
                     help="N > 1: the detections' all-gather on each step's own stream, or on one "
                          "extra stream")
@@ -111,7 +112,18 @@ def parse():
     ap.add_argument("--probe-forwards", type=int, default=10,
                     help="un-captured forwards timed per head launch for the roofline")
     ap.add_argument("--cpu-frames", type=int, default=4, help="frames timed for the CPU baseline")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.inflight is None:
+        args.inflight = 3 if args.workload == "fusion" else 2
+    return args
+
+
+def side_streams_for(args, world, nf):
+    """The models' side streams: every stream of the process takes one of HIP's 4 hardware
+    queues, so "auto" keeps them only while the pipelines' streams and theirs fit (N = 1, at
+    most 2 pipelines); RCCL's own stream at N > 1 and a third pipeline do not
+    (profiles/r02b_ab_gather_streams.txt, r02c_ab_fusion_inflight3.txt)."""
+    return {"on": True, "off": False, "auto": world == 1 and nf <= 2}[args.side_streams]
 
 
 def init_dist(n):
@@ -442,6 +454,7 @@ def run_fusion(args, rank, world, dev):
     # streams in turn, as in the bev_infer workload: one step's kernel tails and its small
     # latency-bound post-processing / fusion launches overlap the other step's convolutions
     nf = max(1, args.inflight)
+    engine.set_side_streams(side_streams_for(args, world, nf))
     fps = []
     for i in range(nf):
         fp = FusionPipeline(engine if i == 0 else engine.twin(), args.batch, [calib], K=args.K,
@@ -530,7 +543,7 @@ def main():
     # side streams: every stream of the process takes one of HIP's 4 hardware queues; with
     # N > 1 RCCL adds its own stream, so the models run without theirs
     # (profiles/r02b_ab_gather_streams.txt: the N > 1 layout rehearsed with --sim-gather).
-    side = {"on": True, "off": False, "auto": world == 1}[args.side_streams]
+    side = side_streams_for(args, world, nf)
     for p in pipes:
         p.engine.set_side_streams(side)
     if args.serial_heads:
