@@ -280,8 +280,8 @@ def probe_heads(args, pipe, step):
 
 
 def probe_bev(args, pipe, reps=20):
-    """configs[2]: the BEV voxelisation pass alone (filter fused, scatter + gather kernels of
-    sfa_bev_voxelize) on the pipeline's resident sweeps, HIP events on the launching stream,
+    """configs[2]: the BEV voxelisation pass alone (filter fused; sfa_bev_voxelize's binned
+    count / scan / bin / strip kernels) on the pipeline's resident sweeps, HIP events on the launching stream,
     against the HBM roofline: algorithmic bytes = N * 16 (xyzi read) + 3 * 608^2 * 4 (f32 map
     written) per frame; scratch key / count traffic is not algorithmic."""
     if args.workload != "e2e":
@@ -306,7 +306,8 @@ def probe_bev(args, pipe, reps=20):
     ach = algo / (ms * 1e-3) / 1e9
     return {"bound": "hbm", "unit": "GB/s", "achieved": round(ach, 1), "peak": 8000.0,
             "frac": round(ach / 8000.0, 4), "traffic": None,
-            "kernel": "sfa_bev_voxelize (SFA_BEV_RAW: filter fused; bev_scatter_kernel + bev_gather_kernel)",
+            "kernel": "sfa_bev_voxelize (SFA_BEV_RAW: filter fused; bev_bin_count / bev_bin_scan / bev_bin / "
+                      "bev_strip kernels, 8-row strips reduced in LDS)",
             "us_per_batch": round(1e3 * ms, 1), "points_per_batch": npts,
             "algorithmic_bytes_per_batch": algo,
             "measured": "HIP events around %d back-to-back voxelisations of the step's %d sweeps, "
@@ -386,10 +387,10 @@ def run_stream(args, rank, world, dev):
     from sfa_hip.stream import StreamingDetector
     arch = _lib.make_arch(DEFAULT_HEADS)
     sd = synthetic.synthetic_state_dict(_lib.state_layout(arch), seed=0)
-    # several pipelines in flight + the copy stream: no side streams, so every stream keeps a
-    # hardware queue of its own (profiles/r02b_stream_side_streams.txt)
-    engine = KfpnEngine(arch, pack_state_dict(sd, arch), dev,
-                        math=MATHS[args.math], side_streams=args.stream_inflight < 2)
+    # several pipelines in flight + the copy stream: no side streams ("auto"), so every stream
+    # keeps a hardware queue of its own (profiles/r02b_stream_side_streams.txt)
+    side = {"on": True, "off": False, "auto": world == 1 and args.stream_inflight < 2}[args.side_streams]
+    engine = KfpnEngine(arch, pack_state_dict(sd, arch), dev, math=MATHS[args.math], side_streams=side)
     tmp = tempfile.mkdtemp(prefix=f"sfa_bins_r{rank}_", dir="/tmp")
     try:
         files = []
