@@ -3,7 +3,10 @@
 // Reference: data_process/kitti_data_utils.py:228-251 (filter),
 //            data_process/kitti_bev_utils.py:22-55 (makeBEVMap).
 //
-// Two passes, HBM/atomic bound (SURVEY §8(a) row a1'):
+// Default: the binned path (count / scan / bin / strip kernels below): points binned by 8-row
+// strips of the map, each strip's top keys and counts reduced in LDS. For batches whose points
+// do not fit the scratch as records, and as SFA_BEV_ATOMIC=1, the global-atomic path:
+// two passes, HBM/atomic bound (SURVEY §8(a) row a1'):
 //   pass 1 (one thread per point): inclusive f32 box test, z' = z - minZ (f32),
 //     cell = (floor(x/D), trunc(floor(y/D) + 304.5)) with IEEE f32 division,
 //     atomicMax of a 64-bit key (bits(z') << 32 | ~index) — z' >= +0 so the
