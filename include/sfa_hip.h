@@ -59,6 +59,10 @@ const char* sfa_last_error_string(void);
  *                 back view of demo_2_sides.py with boundary_back)
  * scratch         device, sfa_bev_scratch_size(batch) bytes, ZERO on first use;
  *                 every call leaves it zeroed again.
+ * Kernels: points binned by 8-row strips of the map and reduced in LDS while the
+ * batch's points fit the scratch as 16-B records (~277 k per frame of scratch);
+ * otherwise (or with env SFA_BEV_ATOMIC=1) device-scope atomics on a per-cell scratch.
+ * Both give the same bits.
  */
 #define SFA_BEV_MAX_BATCH 64
 enum sfa_bev_layout { SFA_BEV_NCHW3_F32 = 0, SFA_BEV_NCHW3_F64 = 1, SFA_BEV_NHWC4_F32 = 2 };
