@@ -304,8 +304,16 @@ def probe_bev(args, pipe, reps=20):
     npts = int(pipe.offsets[-1])
     algo = npts * 16 + pipe.B * 3 * 608 * 608 * 4
     ach = algo / (ms * 1e-3) / 1e9
+    traffic = None  # PMC HBM bytes per call (tools/pmc_bev.sh), for the configuration it was measured on
+    import glob
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_bev.json")))
+    if files and pipe.B == 16:
+        with open(files[-1]) as f:
+            traffic = int(json.load(f)["bev_hbm_bytes_per_call"])
     return {"bound": "hbm", "unit": "GB/s", "achieved": round(ach, 1), "peak": 8000.0,
-            "frac": round(ach / 8000.0, 4), "traffic": None,
+            "frac": round(ach / 8000.0, 4), "traffic": traffic,
+            "traffic_basis": "PMC 2 x FETCH_SIZE + WRITE_SIZE of one call (profiles/r*_pmc_bev.json): points read "
+                             "twice (count + bin), 16-B records written and read, the NHWC4 map's 4th channel",
             "kernel": "sfa_bev_voxelize (SFA_BEV_RAW: filter fused; bev_bin_count / bev_bin_scan / bev_bin / "
                       "bev_strip kernels, 8-row strips reduced in LDS)",
             "us_per_batch": round(1e3 * ms, 1), "points_per_batch": npts,

@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""HBM bytes of one sfa_bev_voxelize call (the binned path's count / scan / bin / strip kernels)
+from tools/pmc_bev.sh output -> JSON for profiles/. FETCH_SIZE doubled and WRITE_SIZE as is
+(gfx950 corrections, MI355X_MICROARCH.md §HBM); the last call of the run is summarised.
+
+  python tools/pmc_bev_summary.py gpurun_out/pmc_bev profiles/r02c_pmc_bev.json"""
+import csv, collections, json, os, re, sys
+
+base, out = sys.argv[1], sys.argv[2]
+KERNELS = ("bev_bin_count_kernel", "bev_bin_scan_kernel", "bev_bin_kernel", "bev_strip_kernel")
+
+
+def load(p, counter):
+    rows = collections.OrderedDict()
+    for r in csv.DictReader(open(os.path.join(base, p, "run_counter_collection.csv"))):
+        name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "")
+        if not any(k + "<" in name or name.endswith(k) for k in KERNELS) or r["Counter_Name"] != counter:
+            continue
+        d = int(r["Dispatch_Id"])
+        e = rows.setdefault(d, {"name": name, "dur_ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), "v": 0.0})
+        e["v"] += float(r["Counter_Value"])
+    return list(rows.values())
+
+
+fetch, write = load("p1", "FETCH_SIZE"), load("p2", "WRITE_SIZE")
+# the last call: the last 4 dispatches (count, scan, bin, strip) of each pass
+f4, w4 = fetch[-4:], write[-4:]
+assert [r["name"] for r in f4] == [r["name"] for r in w4], (f4, w4)
+per = [{"kernel": f["name"], "us": f["dur_ns"] / 1e3, "fetch_MB": 2 * f["v"] * 1024 / 1e6,
+        "write_MB": w["v"] * 1024 / 1e6} for f, w in zip(f4, w4)]
+total = sum(r["fetch_MB"] + r["write_MB"] for r in per) * 1e6
+res = {"bev_hbm_bytes_per_call": int(total), "per_kernel": per,
+       "method": "rocprofv3 --kernel-trace --pmc (FETCH_SIZE, WRITE_SIZE passes), bench.py --workload e2e --no-graph; "
+                 "HBM = 2*FETCH_SIZE + WRITE_SIZE (KiB), last sfa_bev_voxelize call (16 sweeps)"}
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps(res, indent=1))
