@@ -140,26 +140,36 @@ __global__ void __launch_bounds__(256) upsample2x_bilinear_kernel(const float4* 
 // Planar level buffers: Lk[ch][b][y][x] (ch over all heads, forward order).
 // Level 0 is at (h/2, w/2) and resized by nearest (src = dst // 2, F.interpolate
 // default mode with an exact 0.5 scale).
-// grid (ceil(h * w / 256), B, channels): 32-bit index math.
+// grid (ceil(h * w / 4 / 256), B, channels), 4 pixels per thread: 32-bit index math.
 __global__ void __launch_bounds__(256) kfpn_combine_kernel(const float* __restrict__ L0,
                                                            const float* __restrict__ L1,
                                                            const float* __restrict__ L2,
                                                            KfpnOut o, int B, int h, int w) {
+  // every element by the same rounding sequence (no contraction), 4 consecutive pixels of a row
+  // per thread (w % 4 == 0, checked at launch): float4 loads of levels 1 / 2 and of the output,
+  // one float2 of level 0 (nearest: pixels 4q .. 4q + 3 read level-0 columns 2q, 2q + 1)
+#pragma clang fp contract(off)
   const int hw = h * w;
-  const int p = blockIdx.x * 256 + threadIdx.x;
+  const int p = (blockIdx.x * 256 + threadIdx.x) * 4;
   if (p >= hw) return;
   const int b = blockIdx.y, ch = blockIdx.z;
   const int yy = p / w, xx = p - yy * w;
   const int h0 = h / 2, w0 = w / 2;
-  const float v0 = L0[((size_t)ch * B + b) * (h0 * w0) + (yy >> 1) * w0 + (xx >> 1)];
-  const float v1 = L1[((size_t)ch * B + b) * hw + p];
-  const float v2 = L2[((size_t)ch * B + b) * hw + p];
-  // softmax over the stacked last dim (torch: max-subtract, exp, sum, divide).
-  const float mx = fmaxf(fmaxf(v0, v1), v2);
-  const float e0 = expf(v0 - mx), e1 = expf(v1 - mx), e2 = expf(v2 - mx);
-  const float sum = e0 + e1 + e2;
-  const float w0_ = e0 / sum, w1_ = e1 / sum, w2_ = e2 / sum;
-  const float r = v0 * w0_ + v1 * w1_ + v2 * w2_;
+  const float2 l0 = *reinterpret_cast<const float2*>(L0 + ((size_t)ch * B + b) * (h0 * w0) + (yy >> 1) * w0 + (xx >> 1));
+  const float4 l1 = *reinterpret_cast<const float4*>(L1 + ((size_t)ch * B + b) * hw + p);
+  const float4 l2 = *reinterpret_cast<const float4*>(L2 + ((size_t)ch * B + b) * hw + p);
+  const float a0[4] = {l0.x, l0.x, l0.y, l0.y}, a1[4] = {l1.x, l1.y, l1.z, l1.w}, a2[4] = {l2.x, l2.y, l2.z, l2.w};
+  float r[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float v0 = a0[i], v1 = a1[i], v2 = a2[i];
+    // softmax over the stacked last dim (torch: max-subtract, exp, sum, divide).
+    const float mx = fmaxf(fmaxf(v0, v1), v2);
+    const float e0 = expf(v0 - mx), e1 = expf(v1 - mx), e2 = expf(v2 - mx);
+    const float sum = e0 + e1 + e2;
+    const float w0_ = e0 / sum, w1_ = e1 / sum, w2_ = e2 / sum;
+    r[i] = v0 * w0_ + v1 * w1_ + v2 * w2_;
+  }
   // head of this channel
   int hd = 0;
 #pragma unroll
@@ -174,7 +184,7 @@ __global__ void __launch_bounds__(256) kfpn_combine_kernel(const float* __restri
       nc = o.ch[j];
     }
   const int c = ch - o.off[hd];
-  dst[((size_t)b * nc + c) * hw + p] = r;
+  *reinterpret_cast<float4*>(dst + ((size_t)b * nc + c) * hw + p) = make_float4(r[0], r[1], r[2], r[3]);
 }
 
 __global__ void __launch_bounds__(256) sigmoid_clamp_kernel(float* __restrict__ x, long long n) {
@@ -256,7 +266,8 @@ int launch_upsample2x(const float* x, float* y, int B, int H, int W, int C, hipS
 int launch_kfpn(const float* L0, const float* L1, const float* L2, const KfpnOut& o, int B, int h,
                 int w, hipStream_t st) {
   SFA_CHECK_ARG(B <= 65535 && o.total_ch <= 65535, "kfpn: grid too large");
-  hipLaunchKernelGGL(kfpn_combine_kernel, dim3((unsigned)((h * w + 255) / 256), (unsigned)B, (unsigned)o.total_ch),
+  SFA_CHECK_ARG(w % 4 == 0 && h % 2 == 0, "kfpn: head map %dx%d (width must be a multiple of 4)", h, w);
+  hipLaunchKernelGGL(kfpn_combine_kernel, dim3((unsigned)((h * w / 4 + 255) / 256), (unsigned)B, (unsigned)o.total_ch),
                      dim3(256), 0, st, L0, L1, L2, o, B, h, w);
   SFA_LAUNCH_CHECK();
   return SFA_OK;
