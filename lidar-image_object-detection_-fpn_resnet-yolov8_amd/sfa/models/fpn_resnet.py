@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from sfa_hip import _lib
+from sfa_hip import dropin as _dropin
 from sfa_hip.runtime import KfpnEngine, pack_state_dict
 
 BN_MOMENTUM = 0.1
@@ -179,3 +180,7 @@ def get_pose_net(num_layers, heads, head_conv, imagenet_pretrained):
     model = PoseResNet(block_class, layers, heads, head_conv=head_conv)
     model.init_weights(num_layers, pretrained=imagenet_pretrained)
     return model
+
+
+# names of the reference module this drop-in does not define come from the reference
+__getattr__ = _dropin.module_getattr(__name__)

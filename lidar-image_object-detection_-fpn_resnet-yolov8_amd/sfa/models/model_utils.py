@@ -12,6 +12,7 @@ hot path and raises ``NotImplementedError``.
 from __future__ import annotations
 
 from models import fpn_resnet
+from sfa_hip import dropin as _dropin
 
 
 def create_model(configs):
@@ -32,3 +33,7 @@ def create_model(configs):
 def get_num_parameters(model):
     m = model.module if hasattr(model, "module") else model
     return sum(p.numel() for p in m.parameters() if p.requires_grad)
+
+
+# names of the reference module this drop-in does not define come from the reference
+__getattr__ = _dropin.module_getattr(__name__)

@@ -11,6 +11,7 @@ import time
 
 import torch
 
+from sfa_hip import dropin as _dropin
 from sfa_hip.runtime import sigmoid_clamp_
 
 
@@ -29,3 +30,7 @@ def time_synchronized():
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     return time.time()
+
+
+# names of the reference module this drop-in does not define come from the reference
+__getattr__ = _dropin.module_getattr(__name__)
