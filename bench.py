@@ -32,7 +32,7 @@ SFA_ROOT = os.path.join(REPO, "lidar-image_object-detection_-fpn_resnet-yolov8_a
 sys.path.insert(0, SFA_ROOT)
 
 from sfa_hip import _lib, synthetic  # noqa: E402
-from sfa_hip.runtime import (DEFAULT_HEADS, DetectorPipeline, KfpnEngine,  # noqa: E402
+from sfa_hip.runtime import (DEFAULT_BOUNDARY, DEFAULT_HEADS, DetectorPipeline, KfpnEngine,  # noqa: E402
                              pack_state_dict)
 
 # Algorithmic work per frame at 608x608: 53 convs.
@@ -60,7 +60,7 @@ DTYPES = {"fp16x3": "f32 (fp16x3: power-of-two-scaled operands split into 2 fp16
 METRIC = "BEV frames/sec (608x608, bs=16)"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -111,8 +111,7 @@ def parse():
                          "the configuration the roofline probe measures (for rocprof agreement)")
     ap.add_argument("--probe-forwards", type=int, default=10,
                     help="un-captured forwards timed per head launch for the roofline")
-    ap.add_argument("--cpu-frames", type=int, default=4, help="frames timed for the CPU baseline")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     if args.inflight is None:
         args.inflight = 3 if args.workload == "fusion" else 2
     return args
@@ -215,6 +214,79 @@ class StepGraphs:
             self.fns[i]()
         else:
             self.graphs[i].replay()
+
+
+class BevInferBench:
+    """The timed configuration of the bev_infer / e2e workloads: ``--inflight`` pipelines (own
+    model handle, buffers and stream each), forward and decode captured as HIP graphs, the
+    models' side streams per ``side_streams_for``; at N > 1 each step all-gathers its detections.
+    ``one_step(k)`` enqueues step k on stream k % nf.  tests/test_gpu_bench_parity.py builds this
+    same object and checks every frame of it against the oracle."""
+
+    def __init__(self, args, rank, world, dev):
+        self.args, self.rank, self.world, self.dev = args, rank, world, dev
+        nf = self.nf = max(1, args.inflight)
+        pipes = self.pipes = [build_pipeline(dev, args, rank)]
+        for _ in range(nf - 1):  # own model handle each; weights shared (--share-weights) or a copy each
+            pipes.append(build_pipeline(dev, args, rank, pipes[0].engine.twin() if args.share_weights else None))
+        # side streams: every stream of the process takes one of HIP's 4 hardware queues; with
+        # N > 1 RCCL adds its own stream, so the models run without theirs
+        # (profiles/r02b_ab_gather_streams.txt: the N > 1 layout rehearsed with --sim-gather).
+        self.side = side_streams_for(args, world, nf)
+        for p in pipes:
+            p.engine.set_side_streams(self.side)
+        if args.serial_heads:
+            for p in pipes:
+                p.engine.set_probe(_lib.PROBE_SERIAL)
+        self.steps = [StepGraphs(p, not args.no_graph) for p in pipes]
+        self.streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nf - 1)]
+        # --sim-gather (N = 1): a device copy of the detections in place of the all-gather, on the
+        # same stream the gather would use (the N > 1 stream layout rehearsed on one GPU)
+        self.gather = world > 1 or args.sim_gather
+        if self.gather:
+            self.frame_ids = torch.arange(rank * args.batch, (rank + 1) * args.batch, device=dev)
+            self.sim_out = torch.empty_like(pipes[0].dets)
+        self.comm_mode = self.gather and args.gather_stream == "comm"
+        if self.comm_mode:
+            # all-gathers on one extra stream in step order (the same collective order on every
+            # rank); a pipeline's detections are overwritten only after their gather finished
+            self.comm = torch.cuda.Stream()
+            self.step_done = [torch.cuda.Event() for _ in range(nf)]
+            self.comm_done = [torch.cuda.Event() for _ in range(nf)]
+            self.gathered = [0] * nf
+
+    def do_gather(self, dets):
+        if self.world > 1:
+            from sfa_hip import dist as sdist
+            sdist.gather_detections(dets, self.frame_ids)
+        else:
+            self.sim_out.copy_(dets)
+
+    def one_step(self, k, ev=None):
+        i = k % self.nf
+        with torch.cuda.stream(self.streams[i]):
+            if self.comm_mode and self.gathered[i]:
+                self.streams[i].wait_event(self.comm_done[i])
+            if ev is not None:
+                ev[0].record()
+            self.steps[i].run(0)
+            if ev is not None:
+                ev[1].record()
+            self.steps[i].run(1)
+            if ev is not None:
+                ev[2].record()
+            if self.comm_mode:
+                self.step_done[i].record()
+            elif self.gather:
+                # on the step's own stream, in step order (the same collective order on every
+                # rank); RCCL's stream waits for this step only, the other pipeline runs on
+                self.do_gather(self.pipes[i].dets)
+        if self.comm_mode:
+            with torch.cuda.stream(self.comm):
+                self.comm.wait_event(self.step_done[i])
+                self.do_gather(self.pipes[i].dets)
+                self.comm_done[i].record()
+            self.gathered[i] = 1
 
 
 def traffic_per_forward(args):
@@ -357,33 +429,108 @@ def roofline_line(args, heads, forward_roofline, fwd_achieved, peak, peak_basis,
     return line
 
 
-def cpu_baseline(args):
-    """The oracle (torch fp32 CPU restatement of the reference forward + numpy decode),
-    on a bounded sample of the same workload (the reference Python cannot travel)."""
-    sys.path.insert(0, REPO)
-    from oracle import decode_oracle, model_oracle
+def _cpu_model_name():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
+
+
+def _cpu_threads():
+    """Host threads for the CPU baseline: every core this process may run on
+    (len(sched_getaffinity)) -- unless OMP_NUM_THREADS caps the process' CPU
+    share (the GPU box sets it to that share: its affinity mask lists the whole machine)."""
     ncores = len(os.sched_getaffinity(0))
-    threads = max(1, min(ncores, 16))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    threads = min(ncores, int(omp)) if omp.isdigit() and int(omp) > 0 else ncores
+    return threads, ncores
+
+
+def cpu_baseline(args, bench=None):
+    """The CPU leg: the oracle -- the torch fp32 CPU restatement of the reference
+    forward, verified bit-for-bit against reference-generated fixtures, + the numpy restatement
+    of _sigmoid / decode (+ makeBEVMap for e2e) -- on the SAME batch of 16 frames the GPU step
+    processes, 2 warm-ups then the median of 5 batches, all allotted host threads.
+
+    Outside the timed region it doubles as the parity check of the timed configuration: the
+    GPU's logits for those frames (pipeline 0, one more graph replay) against the oracle's
+    (``max_rel_logit_err``, bar 1e-4 * max(1, |ref|)), the GPU's detections against the oracle
+    decode of the GPU's own sigmoid maps (bit-exact: same maps in, same top-K / gathers out), for
+    e2e the GPU BEV maps against the oracle's makeBEVMap (bit-exact)."""
+    sys.path.insert(0, REPO)
+    from oracle import bev_oracle, decode_oracle, model_oracle
+    threads, ncores = _cpu_threads()
     torch.set_num_threads(threads)
     arch = _lib.make_arch(DEFAULT_HEADS)
     sd = model_oracle.state_dict_torch(synthetic.synthetic_state_dict(_lib.state_layout(arch), 0))
-    x = torch.from_numpy(synthetic.synthetic_bev(max(1, args.cpu_frames), seed=1))
+    B = args.batch
+    e2e = args.workload == "e2e"
+    clouds = [synthetic.synthetic_point_cloud(i + 1) for i in range(B)] if e2e else None
+    x_uniform = None if e2e or args.input != "uniform" else torch.from_numpy(synthetic.synthetic_bev(B, seed=1))
+
+    def one_batch():
+        if e2e or x_uniform is None:
+            cl = clouds if clouds is not None else [synthetic.synthetic_point_cloud(i + 1) for i in range(B)]
+            maps = [bev_oracle.makeBEVMap(bev_oracle.get_filtered_lidar(c, DEFAULT_BOUNDARY), DEFAULT_BOUNDARY)
+                    for c in cl]
+            x = torch.from_numpy(np.stack(maps).astype(np.float32))
+        else:
+            maps, x = None, x_uniform
+        with torch.no_grad():
+            out = model_oracle.forward(sd, x)
+        hm = decode_oracle.sigmoid_clamp(out["hm_cen"].numpy())
+        off = decode_oracle.sigmoid_clamp(out["cen_offset"].numpy())
+        dets = decode_oracle.decode(hm, off, out["direction"].numpy(), out["z_coor"].numpy(),
+                                    out["dim"].numpy(), K=args.K)
+        return maps, out, dets
+
+    for _ in range(2):
+        one_batch()
     times = []
-    with torch.no_grad():
-        model_oracle.forward(sd, x[:1])  # warm-up
-        for i in range(x.shape[0]):
-            t0 = time.perf_counter()
-            out = model_oracle.forward(sd, x[i:i + 1])
-            hm = decode_oracle.sigmoid_clamp(out["hm_cen"].numpy())
-            off = decode_oracle.sigmoid_clamp(out["cen_offset"].numpy())
-            decode_oracle.decode(hm, off, out["direction"].numpy(), out["z_coor"].numpy(),
-                                 out["dim"].numpy(), K=args.K)
-            times.append(time.perf_counter() - t0)
+    for _ in range(5):
+        t0 = time.perf_counter()
+        maps, out, dets = one_batch()
+        times.append(time.perf_counter() - t0)
     med = float(np.median(times))
-    return {"value": round(1.0 / med, 3), "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{len(times)} frames of 3x608x608 at bs=1 (median), torch {torch.__version__} "
-                      f"fp32 CPU forward + numpy sigmoid/decode K={args.K}; host "
-                      f"{platform.processor() or platform.machine()}, {threads} threads of {ncores}"}
+    cpu = {"value": round(B / med, 3), "unit": "frames/s", "cores": threads, "kind": "port",
+           "sample": (f"bs={B} batch of the timed workload ({'16 synthetic 132,880-pt sweeps: makeBEVMap + ' if e2e else ''}"
+                      f"3x608x608 forward + sigmoid + decode K={args.K}), 2 warm-ups, median of 5 batches "
+                      f"({med:.2f} s/batch); oracle = torch {torch.__version__} fp32 CPU forward + numpy "
+                      f"decode; host {_cpu_model_name()}, {threads} threads (affinity {ncores} cores, "
+                      f"OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS', 'unset')})")}
+    if bench is None:
+        return cpu, None
+    # parity of the timed configuration (pipeline 0 of the in-flight set, its captured graphs)
+    pipe = bench.pipes[0]
+    torch.cuda.synchronize()
+    bench.one_step(0)
+    torch.cuda.synchronize()
+    worst = 0.0
+    for h, _ in pipe.engine.heads:
+        g = pipe.outs[h].cpu().numpy()
+        r = out[h].numpy()
+        worst = max(worst, float(np.max(np.abs(g - r) / np.maximum(1.0, np.abs(r)))))
+    gd = pipe.dets.cpu().numpy()
+    o = {h: pipe.outs[h].cpu().numpy() for h, _ in pipe.engine.heads}
+    from sfa_hip.runtime import sigmoid_clamp_
+    hm = sigmoid_clamp_(pipe.outs["hm_cen"].clone()).cpu().numpy()
+    off = sigmoid_clamp_(pipe.outs["cen_offset"].clone()).cpu().numpy()
+    ref_dec = decode_oracle.decode(hm, off, o["direction"], o["z_coor"], o["dim"], K=args.K)
+    par = {"frames": B, "max_rel_logit_err": float(f"{worst:.3e}"), "logit_tol": 1e-4,
+           "dets_equal_oracle_decode_of_gpu_maps": bool(np.array_equal(gd, ref_dec)),
+           "max_abs_det_err_vs_oracle_forward": float(f"{float(np.max(np.abs(gd - dets))):.3e}"),
+           "scope": "pipeline 0 of the timed set (HIP graphs, %d in flight, side streams %s, math %s) "
+                    "after the timed region, against the oracle batch timed above" % (bench.nf, bench.side, args.math)}
+    if e2e:
+        gb = pipe.bev[:B].cpu().numpy()
+        ref = np.stack(maps).astype(np.float32).transpose(0, 2, 3, 1)
+        par["bev_equal"] = bool(np.array_equal(gb[..., :3], ref) and not np.any(gb[..., 3]))
+    par["ok"] = bool(worst <= 1e-4 and par["dets_equal_oracle_decode_of_gpu_maps"] and par.get("bev_equal", True))
+    return cpu, par
 
 
 def run_stream(args, rank, world, dev):
@@ -545,72 +692,10 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    nf = max(1, args.inflight)
-    pipes = [build_pipeline(dev, args, rank)]
-    for _ in range(nf - 1):  # own model handle each; weights shared (--share-weights) or a copy each
-        pipes.append(build_pipeline(dev, args, rank, pipes[0].engine.twin() if args.share_weights else None))
-    # side streams: every stream of the process takes one of HIP's 4 hardware queues; with
-    # N > 1 RCCL adds its own stream, so the models run without theirs
-    # (profiles/r02b_ab_gather_streams.txt: the N > 1 layout rehearsed with --sim-gather).
-    side = side_streams_for(args, world, nf)
-    for p in pipes:
-        p.engine.set_side_streams(side)
-    if args.serial_heads:
-        for p in pipes:
-            p.engine.set_probe(_lib.PROBE_SERIAL)
-    steps = [StepGraphs(p, not args.no_graph) for p in pipes]
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nf - 1)]
-    # --sim-gather (N = 1): a device copy of the detections in place of the all-gather, on the
-    # same stream the gather would use (the N > 1 stream layout rehearsed on one GPU)
-    gather = world > 1 or args.sim_gather
-    if gather:
+    bench = BevInferBench(args, rank, world, dev)
+    nf, pipes, steps, side, one_step = bench.nf, bench.pipes, bench.steps, bench.side, bench.one_step
+    if world > 1:
         import torch.distributed as dist
-        from sfa_hip import dist as sdist
-        frame_ids = torch.arange(rank * args.batch, (rank + 1) * args.batch, device=dev)
-        sim_out = torch.empty_like(pipes[0].dets)
-
-        def do_gather(dets):
-            if world > 1:
-                sdist.gather_detections(dets, frame_ids)
-            else:
-                sim_out.copy_(dets)
-
-    if gather and args.gather_stream == "comm":
-        # all-gathers on one extra stream in step order (the same collective order on every
-        # rank); a pipeline's detections are overwritten only after their gather finished
-        comm = torch.cuda.Stream()
-        step_done = [torch.cuda.Event() for _ in range(nf)]
-        comm_done = [torch.cuda.Event() for _ in range(nf)]
-        gathered = [0] * nf
-
-    comm_mode = gather and args.gather_stream == "comm"
-
-    def one_step(k, ev=None):
-        i = k % nf
-        with torch.cuda.stream(streams[i]):
-            if comm_mode and gathered[i]:
-                streams[i].wait_event(comm_done[i])
-            if ev is not None:
-                ev[0].record()
-            steps[i].run(0)
-            if ev is not None:
-                ev[1].record()
-            steps[i].run(1)
-            if ev is not None:
-                ev[2].record()
-            if comm_mode:
-                step_done[i].record()
-            elif gather:
-                # on the step's own stream, in step order (the same collective order on every
-                # rank); RCCL's stream waits for this step only, the other pipeline runs on
-                do_gather(pipes[i].dets)
-        if comm_mode:
-            with torch.cuda.stream(comm):
-                comm.wait_event(step_done[i])
-                do_gather(pipes[i].dets)
-                comm_done[i].record()
-            gathered[i] = 1
-
     for k in range(args.warmup):
         one_step(k)
     torch.cuda.synchronize()
@@ -692,7 +777,7 @@ def main():
         if bev_roof is not None:
             line["bev_roofline"] = bev_roof
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args)
+            line["cpu_baseline"], line["parity"] = cpu_baseline(args, bench)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -61,12 +61,12 @@ const char* sfa_last_error_string(void);
  *                 every call leaves it zeroed again.
  * Kernels: points binned by 8-row strips of the map and reduced in LDS while the
  * batch's points fit the scratch as 16-B records (~277 k per frame of scratch);
- * otherwise (or with env SFA_BEV_ATOMIC=1) device-scope atomics on a per-cell scratch.
- * Both give the same bits.
+ * otherwise (or with flag SFA_BEV_FORCE_ATOMIC: A/B and the equivalence test) device-scope
+ * atomics on a per-cell scratch.  Both give the same bits.
  */
 #define SFA_BEV_MAX_BATCH 64
 enum sfa_bev_layout { SFA_BEV_NCHW3_F32 = 0, SFA_BEV_NCHW3_F64 = 1, SFA_BEV_NHWC4_F32 = 2 };
-enum sfa_bev_flags { SFA_BEV_RAW = 0, SFA_BEV_PREFILTERED = 1, SFA_BEV_FLIP_HW = 2 };
+enum sfa_bev_flags { SFA_BEV_RAW = 0, SFA_BEV_PREFILTERED = 1, SFA_BEV_FLIP_HW = 2, SFA_BEV_FORCE_ATOMIC = 4 };
 
 size_t sfa_bev_scratch_size(int batch);
 int sfa_bev_voxelize(const float* points, const int64_t* frame_offsets, int batch,
@@ -151,6 +151,28 @@ int sfa_model_set_side_streams(sfa_model* model, int on);
 enum sfa_math { SFA_MATH_F32 = 0, SFA_MATH_BF16X6 = 1, SFA_MATH_FP16X3 = 2 };
 int sfa_model_set_math(sfa_model* model, int math);
 int sfa_model_get_math(const sfa_model* model);
+
+/* Kernel-choice options of a model handle (no reference counterpart: A/B runs and the
+ * kernel-equivalence tests).  Every option is a field of the handle, read by the forward when
+ * it enqueues its launches (a captured graph keeps the choice of its capture); nothing on the
+ * launch path reads the environment.  Defaults are the production kernels; at sfa_model_create
+ * the env variable named beside each key seeds it (A/B scripts), sfa_model_set_option
+ * overrides it.  Not concurrently with a forward of this model.
+ *   SFA_OPT_CONV_TUNE        (SFA_TUNE)             bit mask returning conv groups to earlier
+ *                                                   kernels (csrc/conv.hip); 0 = defaults
+ *   SFA_OPT_STEM_PATCH       (SFA_STEM_PATCH)       1: stem + pool from LDS input patches (default)
+ *   SFA_OPT_STEM_POOL_FUSION (SFA_STEM_POOL_FUSION) 1: max-pool fused into the stem (default)
+ *   SFA_OPT_STEM_PATCH_ATOMIC(SFA_STEM_PATCH_ATOMIC)1: patch stem's border cells by atomicMax
+ *   SFA_OPT_FPN_COMMUTE      (SFA_FPN_COMMUTE)      bit mask of FPN levels run commuted (7)
+ *   SFA_OPT_FPN3_SIDE        (SFA_FPN3_SIDE)        1: second side stream (re-creates streams)
+ *   SFA_OPT_STEM_ABL         (SFA_STEM_ABL)         patch-stem timing ablations (wrong results)
+ */
+enum sfa_model_option {
+  SFA_OPT_CONV_TUNE = 0, SFA_OPT_STEM_PATCH = 1, SFA_OPT_STEM_POOL_FUSION = 2,
+  SFA_OPT_STEM_PATCH_ATOMIC = 3, SFA_OPT_FPN_COMMUTE = 4, SFA_OPT_FPN3_SIDE = 5, SFA_OPT_STEM_ABL = 6
+};
+int sfa_model_set_option(sfa_model* model, int key, int value);
+int sfa_model_get_option(const sfa_model* model, int key, int* value);
 
 /* Kernel probe (measurement only; no reference counterpart).  SFA_PROBE_HEADS: every
  * forward NOT being captured into a graph records a timing event before and after each

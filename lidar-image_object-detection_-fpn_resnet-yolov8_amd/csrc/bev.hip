@@ -303,8 +303,10 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
                 SFA_BEV_MAX_BATCH);
   SFA_CHECK_ARG(frame_offsets && boundary && out && scratch, "bev: null argument");
   SFA_CHECK_ARG(out_layout >= 0 && out_layout <= 2, "bev: bad out_layout %d", out_layout);
-  SFA_CHECK_ARG((flags & ~(SFA_BEV_PREFILTERED | SFA_BEV_FLIP_HW)) == 0, "bev: bad flags %d", flags);
+  SFA_CHECK_ARG((flags & ~(SFA_BEV_PREFILTERED | SFA_BEV_FLIP_HW | SFA_BEV_FORCE_ATOMIC)) == 0,
+                "bev: bad flags %d", flags);
   const bool flip = (flags & SFA_BEV_FLIP_HW) != 0;
+  const bool force_atomic = (flags & SFA_BEV_FORCE_ATOMIC) != 0;  // the atomic path (A/B, the equivalence test)
   flags &= SFA_BEV_PREFILTERED;
   BevArgs a;
   int64_t max_n = 0;
@@ -343,8 +345,6 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
   const size_t bin_bytes = align_up((size_t)batch * kStrips * sizeof(unsigned), 256);
   const size_t scratch_bytes = sfa_bev_scratch_size(batch);
   const int64_t total = frame_offsets[batch] - frame_offsets[0];
-  const char* fa = getenv("SFA_BEV_ATOMIC");  // the atomic path (A/B, the equivalence test)
-  const bool force_atomic = fa && strcmp(fa, "0") != 0;
   if (!force_atomic && 3 * bin_bytes < scratch_bytes &&
       (uint64_t)total <= (uint64_t)((scratch_bytes - 3 * bin_bytes) / sizeof(uint4)) && total < (int64_t)0xffffffff) {
     char* sb = reinterpret_cast<char*>(scratch);

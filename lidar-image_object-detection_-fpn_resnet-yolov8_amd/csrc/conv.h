@@ -172,6 +172,11 @@ struct ConvArgs {
   // upsampled x2 (align_corners, source step res_sh / res_sw), or null. bias may be null.
   const float* res_up;
   float res_sh, res_sw;
+  // Host-side kernel choice, copied from the model handle at each launch (never read from the
+  // environment on the launch path): SFA_OPT_CONV_TUNE bits (0 = the defaults, conv.hip) and
+  // SFA_OPT_STEM_ABL (timing ablations of the patch stem; wrong results by design).
+  int tune;
+  int stem_abl;
 };
 
 // Bilinear x2 (align_corners) sample of a half-resolution NHWC tensor at output pixel

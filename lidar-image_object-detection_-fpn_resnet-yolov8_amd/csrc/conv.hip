@@ -71,13 +71,10 @@ static bool strip_ok(const ConvArgs& a) {
 //  * split-K 2 for the 512-wide (layer4) convs, whose 184 tiles cannot fill 256 CUs (-13..16 %);
 //    picked from the width only, so a frame's arithmetic never depends on the batch.
 // conv_x6g_kernel<..., PREC 1> tiles as the fallback.
-// Tuning knob for same-box A/B runs and the kernel-equivalence tests (env SFA_TUNE, 0 = the
-// defaults below). Read at every launch (host side, a few dozen per forward; a captured graph
-// keeps the kernels chosen at capture time).
-static int tune_flags() {
-  const char* e = getenv("SFA_TUNE");
-  return e ? atoi(e) : 0;
-}
+// Tuning knob for same-box A/B runs and the kernel-equivalence tests: ConvArgs::tune, set from
+// the model handle (sfa_model_set_option(SFA_OPT_CONV_TUNE); env SFA_TUNE seeds it when the
+// model is created), 0 = the defaults below. A captured graph keeps the kernels chosen at
+// capture time.
 
 // conv_r3_kernel variants (conv_r3_kernel.h ABL bits): W DMA spread over the column blocks (256),
 // transposed accumulators with float4 / permlane-swap epilogues (2048); heads also s_setprio 1
@@ -104,11 +101,11 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   const bool strip = strip_ok(a) && !sliced;
   if (epilogue == EPI_HEAD) {
     if (a.N == 320) {
-      if (tune_flags() & 64)  // the unpacked head epilogue (A/B)
+      if (a.tune & 64)  // the unpacked head epilogue (A/B)
         rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD & ~65536>(a, st);
-      else if (tune_flags() & 256)  // tap-major K order (A/B)
+      else if (a.tune & 256)  // tap-major K order (A/B)
         rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD & ~524288>(a, st);
-      else if (!(tune_flags() & 4))
+      else if (!(a.tune & 4))
         rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD>(a, st);
       if (!ok(rc)) rc = launch_conv_h3_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2, 1>(a, st);
       if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 320, 32, EPI_HEAD, 1, 16, 3, 0, 320, 1>(a, st);
@@ -116,7 +113,7 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_HEAD, 1, 16, 3, 0, 64, 1>(a, st);
     return rc;
   }
-  if (a.res_up && !(tune_flags() & 32)) {  // FPN skip convs: transposed float4 epilogue, float4 taps
+  if (a.res_up && !(a.tune & 32)) {  // FPN skip convs: transposed float4 epilogue, float4 taps
     if (a.N == 64)
       rc = launch_conv_r3_cfg<128, 64, 32, EPI_STD, 4, 2, R3_FPN>(a, st);
     else if (a.N % 128 == 0)
@@ -125,9 +122,9 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   }
   if (a.N == 64) {
     if (strip) {
-      if (tune_flags() & 16) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3>(a, st);
-      else if (tune_flags() & 1) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 2>(a, st);
-      else if (tune_flags() & 128) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 14>(a, st);  // round-2 A/B
+      if (a.tune & 16) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3>(a, st);
+      else if (a.tune & 1) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 2>(a, st);
+      else if (a.tune & 128) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 14>(a, st);  // round-2 A/B
       else rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, H3S_64>(a, st);
     }
     if (!ok(rc) && a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
@@ -139,13 +136,13 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     ConvArgs b = a;
     b.ksplit = a.part && a.N >= 512 && !sliced && a.bias ? 2 : 1;
     if (strip) {
-      if (tune_flags() & 16)
+      if (a.tune & 16)
         rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
-      else if (tune_flags() & 2)
+      else if (a.tune & 2)
         rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3, 10>(b, st);
       if (!ok(rc)) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, H3S_128>(b, st);
-    } else if (tile_rows(a) >= 50000 && !(tune_flags() & 8)) {  // big-M stride-2 / two-segment: A from registers
-      if (tune_flags() & 256)  // tap-major K order (A/B)
+    } else if (tile_rows(a) >= 50000 && !(a.tune & 8)) {  // big-M stride-2 / two-segment: A from registers
+      if (a.tune & 256)  // tap-major K order (A/B)
         rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY & ~524288>(b, st);
       else
         rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
@@ -153,7 +150,7 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     if (!ok(rc)) {
       // 16x16x32 MFMA form (round 2): -6 % per launch on layer3.0.conv1, +1.2 % end to end
       // (profiles/r02_ab_h3_mf1.txt); SFA_TUNE bit 512 returns to the 32x32x16 form
-      if (tune_flags() & 512)
+      if (a.tune & 512)
         rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
       else
         rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2, 1>(b, st);

@@ -307,7 +307,17 @@ struct sfa_model {
   // keeps every launch on the caller's stream so each head launch has the chip to itself.
   int probe = 0;
   hipEvent_t probe_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  // kernel-choice options (sfa_model_set_option): conv tune bits, patch-stem ablation
+  int tune = 0;
+  int stem_abl = 0;
 };
+
+// A conv's arguments with the model's kernel-choice options (ConvArgs::tune / stem_abl).
+static inline ConvArgs tuned(ConvArgs a, const sfa_model* m) {
+  a.tune = m->tune;
+  a.stem_abl = m->stem_abl;
+  return a;
+}
 
 // The model's side stream(s) and their events, created on the current device; on failure
 // (no device) none, and the forward runs every launch on the caller's stream.
@@ -475,6 +485,10 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   m->w = packed_device;
   m->plan = make_plan(arch);
   m->math = SFA_MATH_FP16X3;
+  // A/B convenience: the environment seeds the options once, here (sfa_model_set_option
+  // overrides them; nothing reads the environment on the launch path)
+  if (const char* e = getenv("SFA_TUNE")) m->tune = atoi(e);
+  if (const char* e = getenv("SFA_STEM_ABL")) m->stem_abl = atoi(e);
   if (const char* e = getenv("SFA_STEM_POOL_FUSION")) m->pool_fusion = strcmp(e, "0") != 0;
   if (const char* e = getenv("SFA_STEM_PATCH")) m->stem_patch = strcmp(e, "0") != 0;
   if (const char* e = getenv("SFA_STEM_PATCH_ATOMIC")) m->stem_atomic = strcmp(e, "0") != 0;
@@ -507,6 +521,50 @@ extern "C" int sfa_model_set_side_streams(sfa_model* model, int on) {
   } else if (on && !model->side) {
     make_side_streams(model);
     SFA_CHECK_ARG(model->side, "set_side_streams: no side stream could be created on this device");
+  }
+  return SFA_OK;
+}
+
+extern "C" int sfa_model_set_option(sfa_model* model, int key, int value) {
+  SFA_CHECK_ARG(model, "set_option: null model");
+  std::lock_guard<std::mutex> lk(model->fork_mu);
+  switch (key) {
+    case SFA_OPT_CONV_TUNE: model->tune = value; break;
+    case SFA_OPT_STEM_PATCH: model->stem_patch = value != 0; break;
+    case SFA_OPT_STEM_POOL_FUSION: model->pool_fusion = value != 0; break;
+    case SFA_OPT_STEM_PATCH_ATOMIC: model->stem_atomic = value != 0; break;
+    case SFA_OPT_FPN_COMMUTE:
+      SFA_CHECK_ARG(value >= 0 && value <= 7, "set_option: FPN_COMMUTE mask %d not in 0..7", value);
+      model->fpn_commute = value;
+      break;
+    case SFA_OPT_FPN3_SIDE:
+      if ((value != 0) != model->fpn3_side) {
+        model->fpn3_side = value != 0;
+        if (model->side) {  // re-create the side streams with / without the second one
+          SFA_HIP_TRY(hipStreamSynchronize(model->side));
+          if (model->side2) SFA_HIP_TRY(hipStreamSynchronize(model->side2));
+          drop_side_streams(model);
+          make_side_streams(model);
+        }
+      }
+      break;
+    case SFA_OPT_STEM_ABL: model->stem_abl = value; break;
+    default: set_error("set_option: unknown key %d", key); return SFA_E_INVALID;
+  }
+  return SFA_OK;
+}
+
+extern "C" int sfa_model_get_option(const sfa_model* model, int key, int* value) {
+  SFA_CHECK_ARG(model && value, "get_option: null argument");
+  switch (key) {
+    case SFA_OPT_CONV_TUNE: *value = model->tune; break;
+    case SFA_OPT_STEM_PATCH: *value = model->stem_patch; break;
+    case SFA_OPT_STEM_POOL_FUSION: *value = model->pool_fusion; break;
+    case SFA_OPT_STEM_PATCH_ATOMIC: *value = model->stem_atomic; break;
+    case SFA_OPT_FPN_COMMUTE: *value = model->fpn_commute; break;
+    case SFA_OPT_FPN3_SIDE: *value = model->fpn3_side; break;
+    case SFA_OPT_STEM_ABL: *value = model->stem_abl; break;
+    default: set_error("get_option: unknown key %d", key); return SFA_E_INVALID;
   }
   return SFA_OK;
 }
@@ -719,12 +777,12 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
         a.part = F(bf.s0);  // the (here unused) unfused stem buffer
         a.part_floats = (size_t)B * H2 * W2 * 64;
       }
-      SFA_RC(launch_stem_patch(a, st));
+      SFA_RC(launch_stem_patch(tuned(a, m), st));
     } else if (pool_fused) {
       SFA_HIP_TRY(hipMemsetAsync(F(bf.p0), 0, (size_t)B * (H2 / 2) * (W2 / 2) * 64 * sizeof(float), st));
-      SFA_RC(launch_conv(a, EPI_POOL, m->math, st));
+      SFA_RC(launch_conv(tuned(a, m), EPI_POOL, m->math, st));
     } else {
-      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
     }
   }
   if (!pool_fused) SFA_RC(launch_maxpool3s2(F(bf.s0), F(bf.p0), B, H2, W2, 64, st));  // :182
@@ -744,7 +802,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       ConvArgs a = conv_args(wb, p.blk[li][0][0], B, oh, ow, t, nullptr, 1);
       a.seg[0] = seg(xcur, B, h, w, cin, 3, stride, 1);
       io(a, xslot, -1, blk_slot(li, 0, 0));
-      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
     }
     {
       ConvArgs a = conv_args(wb, p.blk[li][0][1], B, oh, ow, av, li == 0 ? xcur : nullptr, 1);
@@ -755,20 +813,20 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
         a.seg[1] = seg(xcur, B, h, w, cin, 1, stride, 0);
       }
       io(a, blk_slot(li, 0, 0), li > 0 ? xslot : -1, blk_slot(li, 0, 1));
-      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
     }
     // block 1
     {
       ConvArgs a = conv_args(wb, p.blk[li][1][0], B, oh, ow, t, nullptr, 1);
       a.seg[0] = seg(av, B, oh, ow, planes, 3, 1, 1);
       io(a, blk_slot(li, 0, 1), -1, blk_slot(li, 1, 0));
-      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
     }
     {
       ConvArgs a = conv_args(wb, p.blk[li][1][1], B, oh, ow, lv, av, 1);
       a.seg[0] = seg(t, B, oh, ow, planes, 3, 1, 1);
       io(a, blk_slot(li, 1, 0), -1, blk_slot(li, 1, 1));
-      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
     }
     xcur = lv;
     xslot = blk_slot(li, 1, 1);
@@ -798,7 +856,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       a.wk0 = 0;
       a.seg[0] = seg(x, B, xh, xw, xc, 1, 1, 0);
       io(a, xslot_in, -1, -1);
-      SFA_RC(launch_conv(a, EPI_STD, m->math, fs));
+      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, fs));
     }
     ConvArgs a = conv_args(wb, pc, B, 2 * xh, 2 * xw, out, nullptr, 0);
     a.Kpad = sc;
@@ -809,7 +867,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.res_sh = xh > 1 ? (float)(xh - 1) / (float)(2 * xh - 1) : 0.f;
     a.res_sw = xw > 1 ? (float)(xw - 1) / (float)(2 * xw - 1) : 0.f;
     io(a, skip_slot, -1, out_slot);
-    return launch_conv(a, EPI_STD, m->math, fs);
+    return launch_conv(tuned(a, m), EPI_STD, m->math, fs);
   };
   if (commute_at(0)) {
     SFA_RC(fpn_pair(0, F(bf.l[3]), H / 32, W / 32, 512, blk_slot(3, 1, 1), F(bf.l[2]), 256, blk_slot(2, 1, 1),
@@ -823,7 +881,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       a.seg[0] = seg(F(bf.up1), B, H16, W16, 512, 1, 1, 0);
       a.seg[1] = seg(F(bf.l[2]), B, H16, W16, 256, 1, 1, 0);
       io(a, blk_slot(3, 1, 1), blk_slot(2, 1, 1), AM_FPN + 0);  // up1 = upsample(layer4)
-      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
     }
   }
   SFA_RC(launch_upsample2x(F(bf.c1), F(bf.up2), B, H16, W16, 256, st));
@@ -867,19 +925,20 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     const bool probe = (m->probe & SFA_PROBE_HEADS) && hipStreamIsCapturing(hs, &cap) == hipSuccess &&
                        cap == hipStreamCaptureStatusNone;
     if (probe) SFA_HIP_TRY(hipEventRecord(m->probe_ev[2 * f], hs));
-    SFA_RC(launch_conv(a, EPI_HEAD, m->math, hs));
+    SFA_RC(launch_conv(tuned(a, m), EPI_HEAD, m->math, hs));
     if (probe) SFA_HIP_TRY(hipEventRecord(m->probe_ev[2 * f + 1], hs));
     return SFA_OK;
   };
   // level 0 needs only up_level2: fork it onto the side stream (graph capture follows
   // the event edges), join before apply_kfpn
+  // m->side / m->side2 are read under fork_mu: sfa_model_set_side_streams destroys them under
+  // the same lock, so a concurrent call cannot pull a stream out from under this forward
+  std::unique_lock<std::mutex> fork_lock(const_cast<sfa_model*>(m)->fork_mu);
   int sdev = -1;
   const bool overlap = m->side && !(m->probe & SFA_PROBE_SERIAL) && hipStreamGetDevice(st, &sdev) == hipSuccess &&
                        sdev == m->device;
   const bool side2_on = overlap && m->side2 && m->fpn3_side;
-  std::unique_lock<std::mutex> fork_lock(const_cast<sfa_model*>(m)->fork_mu, std::defer_lock);
   if (overlap) {
-    fork_lock.lock();
     SFA_HIP_TRY(hipEventRecord(m->fork, st));
     SFA_HIP_TRY(hipStreamWaitEvent(m->side, m->fork, 0));
   }
@@ -904,7 +963,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.seg[0] = seg(F(bf.up2), B, H8, W8, 256, 1, 1, 0);
     a.seg[1] = seg(F(bf.l[1]), B, H8, W8, 128, 1, 1, 0);
     io(a, AM_FPN + 0, blk_slot(1, 1, 1), AM_FPN + 1);
-    SFA_RC(launch_conv(a, EPI_STD, m->math, st));
+    SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
   }
   SFA_RC(launch_upsample2x(F(bf.c2), F(bf.up3), B, H8, W8, 128, st));
   // FPN level 3 (-> up_level4) on stream fs
@@ -918,7 +977,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.seg[0] = seg(F(bf.up3), B, H4, W4, 128, 1, 1, 0);
     a.seg[1] = seg(F(bf.l[0]), B, H4, W4, 64, 1, 1, 0);
     io(a, AM_FPN + 1, blk_slot(0, 1, 1), AM_FPN + 2);
-    return launch_conv(a, EPI_STD, m->math, fs);
+    return launch_conv(tuned(a, m), EPI_STD, m->math, fs);
   };
   if (side2_on) {
     // up_level3 is written: FPN level 3 + the level-2 heads on side2, the level-1 heads here,

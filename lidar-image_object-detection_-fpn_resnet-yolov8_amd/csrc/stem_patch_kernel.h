@@ -355,11 +355,7 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
   }
   const int grid = ntiles < ncu ? ntiles : ncu;
   if (grid <= 0) return SFA_OK;
-  static int abl = -1;
-  if (abl < 0) {
-    const char* e = getenv("SFA_STEM_ABL");
-    abl = e ? atoi(e) : 0;
-  }
+  const int abl = a.stem_abl;  // SFA_OPT_STEM_ABL of the model (timing ablations only)
   const dim3 gd((unsigned)grid), bd(stem_patch::NT);
   switch (abl) {
     case 1: hipLaunchKernelGGL(stem_patch_pool_kernel<1>, gd, bd, 0, st, a, ntiles); break;

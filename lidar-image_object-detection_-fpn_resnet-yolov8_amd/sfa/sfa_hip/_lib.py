@@ -23,7 +23,10 @@ SFA_OK = 0
 SFA_MAX_HEADS = 8
 SFA_BEV_MAX_BATCH = 64
 BEV_NCHW3_F32, BEV_NCHW3_F64, BEV_NHWC4_F32 = 0, 1, 2
-BEV_RAW, BEV_PREFILTERED, BEV_FLIP_HW = 0, 1, 2
+BEV_RAW, BEV_PREFILTERED, BEV_FLIP_HW, BEV_FORCE_ATOMIC = 0, 1, 2, 4
+# sfa_model_set_option keys (include/sfa_hip.h sfa_model_option)
+(OPT_CONV_TUNE, OPT_STEM_PATCH, OPT_STEM_POOL_FUSION, OPT_STEM_PATCH_ATOMIC, OPT_FPN_COMMUTE,
+ OPT_FPN3_SIDE, OPT_STEM_ABL) = range(7)
 IN_NCHW3, IN_NHWC4, IN_NCHW3_FLIP_HW = 0, 1, 2
 
 
@@ -75,6 +78,8 @@ _PROTOS = {
 MATH_F32, MATH_BF16X6, MATH_FP16X3 = 0, 1, 2
 _PROTOS["sfa_model_set_math"] = (_c_int, [_vp, _c_int])
 _PROTOS["sfa_model_get_math"] = (_c_int, [_vp])
+_PROTOS["sfa_model_set_option"] = (_c_int, [_vp, _c_int, _c_int])
+_PROTOS["sfa_model_get_option"] = (_c_int, [_vp, _c_int, ctypes.POINTER(_c_int)])
 PROBE_HEADS, PROBE_SERIAL = 1, 2
 _PROTOS["sfa_model_set_probe"] = (_c_int, [_vp, _c_int])
 _PROTOS["sfa_model_set_side_streams"] = (_c_int, [_vp, _c_int])

@@ -7,6 +7,7 @@ capture); every computation on the hot path is a libsfa_hip kernel.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -86,6 +87,17 @@ class KfpnEngine:
         check(lib().sfa_model_set_math(self._h, int(math)), "sfa_model_set_math")
         self.math = int(math)
 
+    def set_option(self, key: int, value: int):
+        """Kernel-choice option of this handle (_lib.OPT_*, include/sfa_hip.h sfa_model_option):
+        A/B runs and the kernel-equivalence tests; the defaults are the production kernels."""
+        with torch.cuda.device(self.device):
+            check(lib().sfa_model_set_option(self._h, int(key), int(value)), "sfa_model_set_option")
+
+    def get_option(self, key: int) -> int:
+        v = ctypes.c_int()
+        check(lib().sfa_model_get_option(self._h, int(key), ctypes.byref(v)), "sfa_model_get_option")
+        return int(v.value)
+
     def set_side_streams(self, on: bool):
         """Side stream for the level-0 heads on (default) or off (sfa_model_set_side_streams):
         off when several forwards are kept in flight beside a copy stream, so the process's
@@ -111,6 +123,9 @@ class KfpnEngine:
         t.set_math(self.math)
         if not self.side_streams:
             t.set_side_streams(False)
+        for key in range(_lib.OPT_STEM_ABL + 1):  # the same kernel choices
+            if t.get_option(key) != self.get_option(key):
+                t.set_option(key, self.get_option(key))
         return t
 
     def set_probe(self, flags: int):
@@ -135,17 +150,26 @@ class KfpnEngine:
     def workspace_bytes(self, B, H, W) -> int:
         return int(lib().sfa_forward_workspace_size(self._h, B, H, W))
 
+    WORKSPACE_CACHE = 2  # streams whose forward workspace stays resident (LRU)
+
     def workspace(self, B, H, W, stream: int = None) -> torch.Tensor:
-        """The forward workspace (activations + fp16x3 max slots) for one stream: forwards on
-        different streams never share one (two concurrent forwards on one stream are ordered
-        by it). One shape per stream stays resident; replacing it first waits for the device,
-        so a forward still running on the old buffer cannot see it reused."""
+        """The forward workspace (activations + fp16x3 max slots) of forwards issued on
+        ``stream`` without an explicit workspace.  Eager forwards on different streams get
+        different buffers; the last ``WORKSPACE_CACHE`` streams keep theirs resident, and
+        evicting or re-shaping an entry first waits for the device, so a forward still running
+        on the old buffer never sees it reused.  Graph captures all issue on torch's capture
+        stream, so graphs captured without an explicit workspace SHARE one buffer: two such
+        graphs must not be replayed concurrently (DetectorPipeline owns its workspace instead)."""
         sk = int(stream) if stream is not None else _lib.stream_ptr(self.device)
-        cur = self._ws.get(sk)
+        cur = self._ws.pop(sk, None)
         if cur is not None and cur[0] == (B, H, W):
+            self._ws[sk] = cur  # most recently used last
             return cur[1]
-        if cur is not None:
+        if cur is not None or len(self._ws) >= self.WORKSPACE_CACHE:
             torch.cuda.synchronize(self.device)
+            del cur
+            while len(self._ws) >= self.WORKSPACE_CACHE:
+                self._ws.pop(next(iter(self._ws)))
         ws = torch.empty(self.workspace_bytes(B, H, W), dtype=torch.uint8, device=self.device)
         self._ws[sk] = ((B, H, W), ws)
         return ws
@@ -213,8 +237,13 @@ class KfpnEngine:
 class BevVoxelizer:
     """sfa_bev_voxelize with its (self-cleaning) scratch kept resident."""
 
-    def __init__(self, device, max_batch: int = 16):
+    def __init__(self, device, max_batch: int = 16, force_atomic: bool = None):
+        """force_atomic: the global-atomic kernels instead of the binned ones (same bits; A/B),
+        default from env SFA_BEV_ATOMIC read once here (flag SFA_BEV_FORCE_ATOMIC per call)."""
         self.device = torch.device(device)
+        if force_atomic is None:
+            force_atomic = os.environ.get("SFA_BEV_ATOMIC", "0") not in ("", "0")
+        self.force_atomic = bool(force_atomic)
         self.max_batch = 0
         self.scratch = None
         self._grow(max_batch)
@@ -246,6 +275,8 @@ class BevVoxelizer:
                 dt = torch.float64 if layout == _lib.BEV_NCHW3_F64 else torch.float32
                 out = torch.empty((B, 3, 608, 608), dtype=dt, device=self.device)
         offs_c = (ctypes.c_int64 * (B + 1))(*offs.tolist())
+        if self.force_atomic:
+            flags |= _lib.BEV_FORCE_ATOMIC
         check(lib().sfa_bev_voxelize(points.data_ptr() if points.numel() else None, offs_c, B,
                                      _boundary_arr(boundary), flags, layout, out.data_ptr(),
                                      self.scratch.data_ptr(),
@@ -409,9 +440,10 @@ class DetectorPipeline:
         self.points = _require_gpu_tensor(points, "load_points")
         self.offsets = np.concatenate([offs, np.full(self.B + 1 - offs.size, offs[-1], np.int64)])
 
-    def run(self, bev_done=None):
+    def run(self, bev_done=None, _eager=False):
         """Enqueue the step; ``bev_done`` (torch.cuda.Event) is recorded once the points have
-        been consumed (after voxelisation)."""
+        been consumed (after voxelisation).  With ``capture_infer()`` done, the forward + decode
+        part replays that graph (``_eager`` forces the eager launches: capture() uses it)."""
         st = _lib.stream_ptr(self.dev)
         if self.with_bev:
             self.vox(self.points, self.offsets, boundary=self.boundary, layout=_lib.BEV_NHWC4_F32,
@@ -422,7 +454,7 @@ class DetectorPipeline:
                          out=self.bev[self.B:], stream=st)
             if bev_done is not None:
                 bev_done.record(torch.cuda.current_stream(self.dev))
-        if self.infer_graph is not None:
+        if self.infer_graph is not None and not _eager:
             self.infer_graph.replay()
             return self.dets
         return self._infer(st)
@@ -443,11 +475,11 @@ class DetectorPipeline:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                self.run()  # warm (module load, lazy init) outside capture
+                self.run(_eager=True)  # warm (module load, lazy init) outside capture
             torch.cuda.current_stream().wait_stream(s)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self.run()
+                self.run(_eager=True)  # the kernels themselves, never a nested graph launch
             self.graph = g
         return g
 

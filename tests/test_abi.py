@@ -174,7 +174,7 @@ def test_argument_errors_before_any_launch():
     offs = (ctypes.c_int64 * 2)(0, 10)
     bnd = (ctypes.c_double * 6)(0, 50, -25, 25, -2.73, 1.27)
     assert L.sfa_bev_voxelize(p, offs, 0, bnd, 0, 2, p, p, None) == -1
-    assert L.sfa_bev_voxelize(p, offs, 1, bnd, 7, 2, p, p, None) == -1
+    assert L.sfa_bev_voxelize(p, offs, 1, bnd, 8, 2, p, p, None) == -1  # unknown flag bit
     assert L.sfa_bev_scratch_size(16) == 16 * 608 * 608 * 12
     # kernel probe (bench roofline): null model / unknown flags / reading a disabled probe
     ms = (ctypes.c_float * 3)()
@@ -188,6 +188,19 @@ def test_argument_errors_before_any_launch():
         assert L.sfa_model_set_probe(h, _lib.PROBE_SERIAL) == 0  # no events needed
         assert L.sfa_model_probe_times(h, ms, 3) == -1 and b"not enabled" in L.sfa_last_error_string()
         assert L.sfa_model_probe_times(h, ms, 4) == -1
+        # kernel-choice options live in the handle (no env reads on the launch path)
+        v = ctypes.c_int()
+        defaults = {_lib.OPT_CONV_TUNE: 0, _lib.OPT_STEM_PATCH: 1, _lib.OPT_STEM_POOL_FUSION: 1,
+                    _lib.OPT_STEM_PATCH_ATOMIC: 0, _lib.OPT_FPN_COMMUTE: 7, _lib.OPT_FPN3_SIDE: 0,
+                    _lib.OPT_STEM_ABL: 0}
+        for key, val in defaults.items():
+            assert L.sfa_model_get_option(h, key, ctypes.byref(v)) == 0 and v.value == val, key
+        assert L.sfa_model_set_option(h, _lib.OPT_CONV_TUNE, 28) == 0
+        assert L.sfa_model_get_option(h, _lib.OPT_CONV_TUNE, ctypes.byref(v)) == 0 and v.value == 28
+        assert L.sfa_model_set_option(h, _lib.OPT_FPN_COMMUTE, 9) == -1
+        assert L.sfa_model_set_option(h, 99, 0) == -1 and b"unknown key" in L.sfa_last_error_string()
+        assert L.sfa_model_get_option(h, 99, ctypes.byref(v)) == -1
+        assert L.sfa_model_set_option(None, 0, 0) == -1
     finally:
         L.sfa_model_destroy(h)
 

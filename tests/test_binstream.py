@@ -59,3 +59,35 @@ def test_capacity_and_missing_file(tmp_path):
         s.next()
     with BinStream([], 4, 10) as s:
         assert s.next() is None
+
+
+SANITIZERS = {"asan_ubsan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=all"],
+              "tsan": ["-fsanitize=thread"]}
+
+
+@pytest.mark.parametrize("san", sorted(SANITIZERS))
+def test_binstream_under_host_sanitizers(tmp_path, san):
+    """csrc/binstream.cpp (producer thread + pread pool + two-slot state machine) built with
+    ASan + UBSan and with TSan and driven by tests/native/binstream_sanitize.cpp in host mode:
+    batches equal the files' bytes for several batch / reader counts, early destroy, error
+    batches; any sanitizer report fails the run (SURVEY §5 race detection)."""
+    import os
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None or not os.path.isdir("/opt/rocm/include"):
+        pytest.skip("g++ / ROCm headers not available")
+    here = os.path.dirname(os.path.abspath(__file__))
+    csrc = os.path.join(os.path.dirname(here), "lidar-image_object-detection_-fpn_resnet-yolov8_amd", "csrc")
+    exe = str(tmp_path / f"binstream_{san}")
+    cmd = [gxx, "-std=c++17", "-g", "-O1", "-fno-omit-frame-pointer", *SANITIZERS[san],
+           "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include", os.path.join(csrc, "binstream.cpp"),
+           os.path.join(here, "native", "binstream_sanitize.cpp"), "-L/opt/rocm/lib",
+           "-Wl,-rpath,/opt/rocm/lib", "-lamdhip64", "-pthread", "-o", exe]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:verify_asan_link_order=0",
+               TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    r = subprocess.run([exe, str(tmp_path)], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "binstream sanitize ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "WARNING: ThreadSanitizer" not in r.stderr and "ERROR: AddressSanitizer" not in r.stderr

@@ -106,9 +106,9 @@ def test_cpu_input_refused():
 
 
 @pytest.mark.parametrize("flip", [False, True])
-def test_binned_path_equals_atomic_path(gpu, monkeypatch, flip):
+def test_binned_path_equals_atomic_path(gpu, flip):
     """The default binned voxeliser (points binned by 8-row strips, each strip reduced in LDS)
-    gives the bits of the global-atomic one (SFA_BEV_ATOMIC=1) in every layout, flipped or not,
+    gives the bits of the global-atomic one (flag SFA_BEV_FORCE_ATOMIC) in every layout, flipped or not,
     on a ragged batch with a saturated-density cell and an empty frame; both leave the scratch
     zeroed."""
     from sfa_hip import synthetic
@@ -125,14 +125,11 @@ def test_binned_path_equals_atomic_path(gpu, monkeypatch, flip):
     vox = runtime.BevVoxelizer(gpu, len(clouds))
     flags = _lib.BEV_RAW | (_lib.BEV_FLIP_HW if flip else 0)
     for layout in (_lib.BEV_NCHW3_F64, _lib.BEV_NCHW3_F32, _lib.BEV_NHWC4_F32):
-        monkeypatch.delenv("SFA_BEV_ATOMIC", raising=False)
         binned = vox(pts, offs, gc.BOUNDARY, layout=layout, flags=flags).cpu().numpy()
         assert int(vox.scratch.count_nonzero()) == 0
-        monkeypatch.setenv("SFA_BEV_ATOMIC", "1")
-        atomic = vox(pts, offs, gc.BOUNDARY, layout=layout, flags=flags).cpu().numpy()
+        atomic = vox(pts, offs, gc.BOUNDARY, layout=layout, flags=flags | _lib.BEV_FORCE_ATOMIC).cpu().numpy()
         assert int(vox.scratch.count_nonzero()) == 0
         np.testing.assert_array_equal(binned, atomic)
-    monkeypatch.delenv("SFA_BEV_ATOMIC", raising=False)
     f64 = vox(pts, offs, gc.BOUNDARY, layout=_lib.BEV_NCHW3_F64).cpu().numpy()
     for i, c in enumerate(clouds):
         exp = bev_oracle.makeBEVMap(bev_oracle.get_filtered_lidar(c, gc.BOUNDARY), gc.BOUNDARY)

@@ -21,11 +21,11 @@ pytestmark = pytest.mark.gpu
 def test_fusion_pipeline_matches_oracles(golden, gpu, conf_source, nms):
     """nms="gaussian": the README's Gaussian soft-NMS (README.md:250-261) on the fused lists
     instead of the greedy NMS: confidences within 1e-14 rel. of the oracle (device vs numpy exp)."""
-    B = 4
+    B = 8  # BASELINE configs[4] batch
     arch = _lib.make_arch(gc.HEADS)
     eng = runtime.KfpnEngine(arch, runtime.pack_state_dict(gc.state_dict_np(golden.model), arch), gpu)
     cal = project_cases.calibs()
-    names = ["avg", "seq", "avg", "seq"]
+    names = ["avg", "seq"] * (B // 2)
     calibs = [runtime.make_calib(cal[n]["V2C"], cal[n]["R0"], cal[n]["P2"], cal[n]["img_shape"])
               for n in names]
     clouds = [synthetic.synthetic_point_cloud(s) for s in range(1, B + 1)]

@@ -12,7 +12,7 @@ import pytest
 import torch
 
 import golden_cases as gc
-from sfa_hip import synthetic
+from sfa_hip import _lib, synthetic
 
 pytestmark = pytest.mark.gpu
 
@@ -176,34 +176,36 @@ def test_forward_608_math_modes(golden, gpu, math):
         assert e <= TOL
 
 
-def test_stem_pool_fusion_bit_exact(golden, gpu, monkeypatch):
+def test_stem_pool_fusion_bit_exact(golden, gpu):
     """fp16x3 stem with the max-pool fused into its epilogue (tile-border cells combined by
     atomicMax) == stem conv + maxpool3s2_kernel, bit for bit over the whole forward."""
     x = torch.from_numpy(synthetic.synthetic_bev(3, 160, 192, seed=11)).to(gpu)
     outs = []
-    monkeypatch.setenv("SFA_STEM_PATCH", "0")  # the implicit-GEMM stem (same K order as unfused)
-    for flag in ("1", "0"):
-        monkeypatch.setenv("SFA_STEM_POOL_FUSION", flag)
-        model = make_model(golden, gpu)  # the flag is read when the native model is created
-        model._engine(gpu).set_math(_math("fp16x3"))
+    for flag in (1, 0):
+        model = make_model(golden, gpu)
+        eng = model._engine(gpu)
+        eng.set_option(_lib.OPT_STEM_PATCH, 0)  # the implicit-GEMM stem (same K order as unfused)
+        eng.set_option(_lib.OPT_STEM_POOL_FUSION, flag)
+        eng.set_math(_math("fp16x3"))
         with torch.no_grad():
             outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
     for h in gc.HEADS:
         np.testing.assert_array_equal(outs[0][h], outs[1][h])
 
 
-def test_stem_patch_side_buffer_bit_exact(golden, gpu, monkeypatch):
+def test_stem_patch_side_buffer_bit_exact(golden, gpu):
     """Patch stem: tile-border pooled cells through the owner tile + side buffer +
     stem_pool_merge_kernel (default) == atomicMax into the zeroed pooled buffer
-    (SFA_STEM_PATCH_ATOMIC=1), bit for bit over the whole forward. 160x192 -> an 80x96 conv
+    (OPT_STEM_PATCH_ATOMIC), bit for bit over the whole forward. 160x192 -> an 80x96 conv
     output = 5x6 tiles of 16x16, so the up, left and up-left (corner) merges all run."""
     x = torch.from_numpy(synthetic.synthetic_bev(3, 160, 192, seed=23)).to(gpu)
     outs = []
-    monkeypatch.setenv("SFA_STEM_PATCH", "1")
-    for flag in ("0", "1"):
-        monkeypatch.setenv("SFA_STEM_PATCH_ATOMIC", flag)
-        model = make_model(golden, gpu)  # the flag is read when the native model is created
-        model._engine(gpu).set_math(_math("fp16x3"))
+    for flag in (0, 1):
+        model = make_model(golden, gpu)
+        eng = model._engine(gpu)
+        eng.set_option(_lib.OPT_STEM_PATCH, 1)
+        eng.set_option(_lib.OPT_STEM_PATCH_ATOMIC, flag)
+        eng.set_math(_math("fp16x3"))
         with torch.no_grad():
             outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
     for h in gc.HEADS:
@@ -211,16 +213,16 @@ def test_stem_patch_side_buffer_bit_exact(golden, gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("hw", [(160, 192), (608, 608)])
-def test_stem_patch_matches_gather_stem(golden, gpu, monkeypatch, hw):
+def test_stem_patch_matches_gather_stem(golden, gpu, hw):
     """fp16x3 stem + pool from LDS input patches (stem_patch_kernel.h: K laid out with kw
     padded to 8, so its f32 sums run in a different order) == the implicit-GEMM fused stem
     to f32 rounding; both within the 1e-4 bar of the CPU reference."""
     from oracle import model_oracle
     x = torch.from_numpy(synthetic.synthetic_bev(2, hw[0], hw[1], seed=17)).to(gpu)
     outs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("SFA_STEM_PATCH", flag)
+    for flag in (1, 0):
         model = make_model(golden, gpu)
+        model._engine(gpu).set_option(_lib.OPT_STEM_PATCH, flag)
         model._engine(gpu).set_math(_math("fp16x3"))
         with torch.no_grad():
             outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
@@ -236,16 +238,16 @@ def test_stem_patch_matches_gather_stem(golden, gpu, monkeypatch, hw):
         assert e <= 1e-4, h
 
 
-def test_fpn_commute_matches_concat_conv(golden, gpu, monkeypatch):
+def test_fpn_commute_matches_concat_conv(golden, gpu):
     """fp16x3 FPN 1x1 convs run as up(W_a x) + W_b skip + b (K-sliced weights, half-res
     residual upsampled in the epilogue) == the conv over cat(up(x), skip), to f32 rounding;
     both within the 1e-4 bar of the CPU reference."""
     from oracle import model_oracle
     x = torch.from_numpy(synthetic.synthetic_bev(2, 160, 192, seed=13)).to(gpu)
     outs = []
-    for flag in ("7", "0"):
-        monkeypatch.setenv("SFA_FPN_COMMUTE", flag)
+    for flag in (7, 0):
         model = make_model(golden, gpu)
+        model._engine(gpu).set_option(_lib.OPT_FPN_COMMUTE, flag)
         model._engine(gpu).set_math(_math("fp16x3"))
         with torch.no_grad():
             outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
@@ -259,18 +261,18 @@ def test_fpn_commute_matches_concat_conv(golden, gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("hw", [(160, 192), (96, 96)])
-def test_round2_kernels_match_round1(golden, gpu, monkeypatch, hw):
+def test_round2_kernels_match_round1(golden, gpu, hw):
     """Round-2 conv kernels (conv_r3_kernel for the heads and the big-M non-strip convs, the
-    transposed / pre-split strip kernel) == the round-1 kernels (SFA_TUNE=28: conv_h3_kernel,
+    transposed / pre-split strip kernel) == the round-1 kernels (OPT_CONV_TUNE 28: conv_h3_kernel,
     the plain strip kernel) to f32 rounding (the head epilogue sums the 1x1 conv in another
     order), both within the 1e-4 bar of the CPU reference. Odd sizes: partial last row tiles,
     tiles spanning two frames, every image border of the register-A loads."""
     from oracle import model_oracle
     x = torch.from_numpy(synthetic.synthetic_bev(3, hw[0], hw[1], seed=29)).to(gpu)
     outs = []
-    for flag in ("0", "28"):
-        monkeypatch.setenv("SFA_TUNE", flag)
+    for flag in (0, 28):
         model = make_model(golden, gpu)
+        model._engine(gpu).set_option(_lib.OPT_CONV_TUNE, flag)
         model._engine(gpu).set_math(_math("fp16x3"))
         with torch.no_grad():
             outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
@@ -286,14 +288,14 @@ def test_round2_kernels_match_round1(golden, gpu, monkeypatch, hw):
         assert e <= 1e-4, h
 
 
-@pytest.mark.parametrize("tune", ["0", "28", "32", "256", "512"])
-def test_batch_invariance_608(golden, gpu, monkeypatch, tune):
+@pytest.mark.parametrize("tune", [0, 28, 32, 256, 512])
+def test_batch_invariance_608(golden, gpu, tune):
     """At the full 608x608 size (every kernel path of the bench: r3 heads, strip convs, FPN skip
     convs, r3 body convs (M >= 50000 needs >= 9 frames), split-K layer4): frames 7, 8 of a batch
     of 10 == the same frames as a batch of 2 (their rows sit at other offsets within the tiles),
     and a repeated forward is bit-identical (no cross-frame leakage, no nondeterminism)."""
-    monkeypatch.setenv("SFA_TUNE", tune)
     model = make_model(golden, gpu)
+    model._engine(gpu).set_option(_lib.OPT_CONV_TUNE, tune)
     model._engine(gpu).set_math(_math("fp16x3"))
     x = torch.from_numpy(synthetic.synthetic_bev(10, 608, 608, seed=31)).to(gpu)
     with torch.no_grad():

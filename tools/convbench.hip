@@ -322,6 +322,8 @@ int main(int argc, char** argv) {
     }
     ConvArgs a;
     memset(&a, 0, sizeof a);
+    a.tune = getenv("SFA_TUNE") ? atoi(getenv("SFA_TUNE")) : 0;  // kernel choice (the model's OPT_CONV_TUNE)
+    a.stem_abl = getenv("SFA_STEM_ABL") ? atoi(getenv("SFA_STEM_ABL")) : 0;
     a.nseg = 1;
     make_seg(a.seg[0], x, sh.B, sh.H, sh.W, sh.C, sh.k, sh.stride, sh.pad);
     a.w = w;
