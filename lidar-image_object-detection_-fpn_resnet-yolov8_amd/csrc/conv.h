@@ -113,6 +113,20 @@ __device__ __forceinline__ float amax_frame_scale(const unsigned* const (&amax)[
   return __uint_as_float((unsigned)(127 + 13 - e) << 23);
 }
 
+// The same scale from the float bits of a max |x| (a tile's own maximum).
+__device__ __forceinline__ float amax_scale_bits(unsigned mb, float& sinv) {
+  if (mb == 0 || mb >= 0x7f800000u) {
+    sinv = 1.f;
+    return 1.f;
+  }
+  int e = (int)(mb >> 23) - 127;
+  e = e < -100 ? -100 : (e > 100 ? 100 : e);
+  sinv = __uint_as_float((unsigned)(127 - 13 + e) << 23);
+  return __uint_as_float((unsigned)(127 + 13 - e) << 23);
+}
+
+enum StemInput { STEM_IN_NHWC4 = 0, STEM_IN_NCHW3 = 1, STEM_IN_NCHW3_FLIP = 2 };
+
 // Producer side of a conv epilogue (rows m of the output, P = OH * OW rows per frame):
 // frames fb0 and fb0 + 1 are reduced over the block, rows of later frames (blocks taller
 // than a frame: small maps) are committed one by one.
@@ -177,6 +191,10 @@ struct ConvArgs {
   // SFA_OPT_STEM_ABL (timing ablations of the patch stem; wrong results by design).
   int tune;
   int stem_abl;
+  // Patch stem input (stem_patch_kernel.h): STEM_IN_NHWC4 (the voxeliser's layout), STEM_IN_NCHW3
+  // (the reference's (B, 3, H, W)), STEM_IN_NCHW3_FLIP (read as torch.flip(x, [2, 3])); every
+  // 16 x 16 output tile scales its fp16x3 patch by its own max |x| (no layout / amax pass).
+  int stem_in;
 };
 
 // Bilinear x2 (align_corners) sample of a half-resolution NHWC tensor at output pixel

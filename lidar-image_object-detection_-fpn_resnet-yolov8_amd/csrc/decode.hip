@@ -14,6 +14,22 @@
 //   (value desc, class*K + rank asc) — torch's second topk — and the K winners
 //   gather offset / direction / z / dim at their pixel into (K, 10) rows.
 // Integer selection is exact; outputs are bit-exact given identical maps.
+//
+// Round 3 — band-parallel form (the default whenever a band tile fits LDS): the 48 (frame,
+// class) workgroups above left 208 of 256 CUs idle for ~60 us.  Now each class map is cut into
+// S row bands (S = 8 at 152x152, K = 50: 384 workgroups of 256 threads), and
+//   decode_band_topk_kernel: one workgroup per (band, class, frame) stages its R rows + a
+//     1-row halo in LDS, applies sigmoid + clamp, runs the 3x3 peak test and selects the band's
+//     top min(K, band) peaks by (value desc, index asc) with the same radix select + ordered
+//     tie scan, written as a list sorted in that order (padded to K with sentinels);
+//   decode_band_merge_gather_kernel: one workgroup per frame merges the C*S sorted band lists
+//     pairwise in log2(C*S) rounds (each merge truncated to K) in (value desc, class asc,
+//     index asc) order and gathers the K winners.
+// Equivalence with the reference's two topk stages: an entry in the final top K has fewer than
+// K entries before it in (value desc, class asc, index asc) order, hence fewer than K of its
+// own class (or band) before it in that class's (value desc, index asc) order, so it survives
+// every per-class (per-band) top-K; and torch's second stage orders equal values by class*K +
+// rank = (class asc, index asc).  Same results bit for bit as the one-block-per-class kernels.
 #include "common.h"
 
 namespace sfa {
@@ -271,13 +287,341 @@ __global__ void __launch_bounds__(256) decode_merge_gather_kernel(
   }
 }
 
+constexpr int kBandThreads = 512;
+constexpr int kBandWaves = kBandThreads / 64;
+constexpr int kBandMaxTile = 8192;   // LDS floats of a band tile ((R + 2) x (W + 2), -inf border)
+constexpr int kBandMaxIPT = 8;       // band pixels per thread
+constexpr int kBandMaxLoads = 16;    // staged tile floats per thread
+constexpr int kMergeMax = 4096;      // C * S * K candidates ranked per frame
+
+// Block-wide exclusive scan of one int per thread (kBandWaves waves).
+__device__ int band_excl_scan(int v, int* wsum /*[kBandWaves]*/) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  int before = 0;
+#pragma unroll
+  for (int w = 0; w < kBandWaves; ++w) before += w < wave ? wsum[w] : 0;
+  return before + x - v;
+}
+
+// ABL (timing ablations, tools/decodebench.hip only; results wrong): 1 = no sigmoid, 2 = no peak
+// test, 4 = no radix select (nothing selected), 8 = no band sort
+//
+// grid (S, C, B): band s = rows [s*R, min(H, s*R + R)) of class map (b, c).  The band's rows
+// plus a 1-row halo are staged in LDS with a -inf border (max_pool2d's padding: rows outside
+// the map and columns -1 / W), so the 3x3 peak test is nine unconditional reads.  Writes the
+// band's top min(K, band pixels) by (value desc, index asc) as a sorted list of K (key, index),
+// padded with sentinels (key 0, index INT_MAX), to bkey / bidx[((b * C + c) * S + s) * K + j].
+template <int ABL = 0>
+__global__ void __launch_bounds__(kBandThreads) decode_band_topk_kernel(
+    const float* __restrict__ hm, int C, int H, int W, int K, int R, int apply_sigmoid,
+    unsigned* __restrict__ bkey, int* __restrict__ bidx) {
+  __shared__ __attribute__((aligned(16))) float tile[kBandMaxTile];
+  __shared__ unsigned hist[256];
+  __shared__ int wsum[kBandWaves];
+  __shared__ int misc[4];
+  __shared__ unsigned sel_key[kDecMaxK];
+  __shared__ int sel_idx[kDecMaxK];
+  const int s = blockIdx.x, c = blockIdx.y, b = blockIdx.z, S = gridDim.x;
+  const int tid = threadIdx.x;
+  const int y0 = s * R, y1 = min(H, y0 + R);
+  const int TW = W + 2;                 // tile row: column -1, 0 .. W-1, W
+  const int n_tile = (y1 - y0 + 2) * TW;  // tile rows y0 - 1 .. y1
+  const float* src = hm + ((size_t)b * C + c) * H * W;
+  {
+    // every load in flight before the first use (the map is read once)
+    float v[kBandMaxLoads];
+#pragma unroll
+    for (int j = 0; j < kBandMaxLoads; ++j) {
+      const int i = tid + j * kBandThreads;
+      const int r = i / TW, x = i - r * TW - 1, y = y0 - 1 + r;
+      const bool in = i < n_tile && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+      v[j] = in ? __builtin_nontemporal_load(src + (size_t)y * W + x) : -INFINITY;
+    }
+#pragma unroll
+    for (int j = 0; j < kBandMaxLoads; ++j) {
+      const int i = tid + j * kBandThreads;
+      if (i < n_tile) {
+        const int r = i / TW, x = i - r * TW - 1, y = y0 - 1 + r;
+        const bool in = (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;  // not the border
+        tile[i] = (in && apply_sigmoid && !(ABL & 1)) ? sigmoid_clamp_f(v[j]) : v[j];
+      }
+    }
+  }
+  __syncthreads();
+  // 3x3 peak test over the band's pixels; each thread owns a contiguous index range so the
+  // tie scan follows flat-index order
+  const int nb = (y1 - y0) * W;  // band pixels
+  const int ipt = (nb + kBandThreads - 1) / kBandThreads;
+  const int i0 = min(tid * ipt, nb), i1 = min(i0 + ipt, nb);
+  unsigned key[kBandMaxIPT];
+  {
+    int r = i0 / W, x = i0 - (i0 / W) * W;  // band row, column (walked incrementally)
+#pragma unroll
+    for (int j = 0; j < kBandMaxIPT; ++j) {
+      unsigned k = 0u;
+      if (i0 + j < i1) {
+        const float* t = tile + (r + 1) * TW + x + 1;  // the pixel; neighbours at +-1, +-TW
+        const float v = t[0];
+        float m = v;
+        if (!(ABL & 2)) {
+          const float a0 = fmaxf(fmaxf(t[-TW - 1], t[-TW]), t[-TW + 1]);
+          const float a1 = fmaxf(t[-1], t[1]);
+          const float a2 = fmaxf(fmaxf(t[TW - 1], t[TW]), t[TW + 1]);
+          m = fmaxf(m, fmaxf(a0, fmaxf(a1, a2)));
+        }
+        k = fkey((m == v) ? v : v * 0.f);  // heat * keep: non-peaks become (signed) zero
+        if (++x == W) {
+          x = 0;
+          ++r;
+        }
+      }
+      key[j] = k;
+    }
+  }
+  const int kk = min(K, nb);  // real candidates of this band
+  // Radix select of the kk-th largest key.
+  unsigned prefix = (ABL & 4) ? 0xffffffffu : 0u, pmask = 0u;
+  int krem = (ABL & 4) ? 0 : kk;
+  for (int pass = 0; pass < ((ABL & 4) ? 0 : 4); ++pass) {
+    const int shift = 24 - 8 * pass;
+    for (int i = tid; i < 256; i += kBandThreads) hist[i] = 0u;
+    __syncthreads();
+    constexpr unsigned kZero = 0x80000000u;  // fkey(0.f): the non-peaks, counted per wave
+    unsigned nzero = 0;
+#pragma unroll
+    for (int j = 0; j < kBandMaxIPT; ++j) {
+      if (i0 + j < i1) {
+        const unsigned k = key[j];
+        if ((k & pmask) == prefix) {
+          if (k == kZero)
+            ++nzero;
+          else
+            atomicAdd(&hist[(k >> shift) & 255u], 1u);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nzero += __shfl_xor(nzero, o, 64);
+    if ((tid & 63) == 0 && nzero) atomicAdd(&hist[(kZero >> shift) & 255u], nzero);
+    __syncthreads();
+    if (tid < 64) {
+      unsigned c4[4];
+      unsigned loc = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        c4[q] = hist[255 - (4 * tid + q)];
+        loc += c4[q];
+      }
+      unsigned x = loc;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned y = __shfl_up(x, o, 64);
+        if (tid >= o) x += y;
+      }
+      unsigned above = x - loc;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (above < (unsigned)krem && above + c4[q] >= (unsigned)krem) {
+          misc[0] = 255 - (4 * tid + q);
+          misc[1] = krem - (int)above;
+        }
+        above += c4[q];
+      }
+    }
+    __syncthreads();
+    prefix |= (unsigned)misc[0] << shift;
+    pmask |= 255u << shift;
+    krem = misc[1];
+    __syncthreads();
+  }
+  const unsigned T = prefix;  // key of the kk-th largest; take krem of the keys == T
+  int nties = 0;
+#pragma unroll
+  for (int j = 0; j < kBandMaxIPT; ++j)
+    if (i0 + j < i1) nties += key[j] == T;
+  if (tid == 0) misc[2] = 0;
+  int tie_rank = band_excl_scan(nties, wsum);
+  __syncthreads();  // misc[2] = 0 visible
+  const int pix0 = y0 * W;  // flat index of the band's first pixel in the class map
+#pragma unroll
+  for (int j = 0; j < kBandMaxIPT; ++j) {
+    if (i0 + j < i1) {
+      const unsigned k = key[j];
+      bool take = k > T;
+      if (k == T) {
+        take = tie_rank < krem;
+        ++tie_rank;
+      }
+      if (take) {
+        const int slot = atomicAdd(&misc[2], 1);
+        sel_key[slot] = k;
+        sel_idx[slot] = pix0 + i0 + j;
+      }
+    }
+  }
+  __syncthreads();
+  // the band's list sorted by (value desc, index asc), then sentinels (key 0, index INT_MAX)
+  // that never rank into the top K: the merge kernel merges these lists
+  const size_t out0 = (((size_t)b * C + c) * S + s) * K;
+  for (int t = tid; t < K; t += kBandThreads) {
+    if (t < kk && !(ABL & 8)) {
+      const unsigned k = sel_key[t];
+      const int ix = sel_idx[t];
+      int r0 = 0, r1 = 0, r2 = 0, r3 = 0;  // four independent chains (LDS latency)
+      int j = 0;
+      for (; j + 4 <= kk; j += 4) {
+        const unsigned k0 = sel_key[j], k1 = sel_key[j + 1], k2 = sel_key[j + 2], k3 = sel_key[j + 3];
+        const int x0 = sel_idx[j], x1 = sel_idx[j + 1], x2 = sel_idx[j + 2], x3 = sel_idx[j + 3];
+        r0 += (k0 > k) || (k0 == k && x0 < ix);
+        r1 += (k1 > k) || (k1 == k && x1 < ix);
+        r2 += (k2 > k) || (k2 == k && x2 < ix);
+        r3 += (k3 > k) || (k3 == k && x3 < ix);
+      }
+      for (; j < kk; ++j) r0 += (sel_key[j] > k) || (sel_key[j] == k && sel_idx[j] < ix);
+      const int rank = r0 + r1 + r2 + r3;
+      bkey[out0 + rank] = k;
+      bidx[out0 + rank] = ix;
+    } else {
+      bkey[out0 + t] = 0u;
+      bidx[out0 + t] = 0x7fffffff;
+    }
+  }
+}
+
+// One workgroup per frame: the C*S*K band candidates (L = C*S sorted lists of K) are merged
+// pairwise, log2(L) rounds, each pair's merge truncated to its first K — the top K of a union
+// of two lists comes from the top K of each — in (value desc, class asc, index asc) order: an
+// entry's place in the merged pair is its own position plus the number of partner entries that
+// precede it (a binary search; equal entries, only the sentinels, break left-first).  The K
+// winners of the last list gather offset / direction / z / dim into (K, 10) rows
+// (decode_merge_gather_kernel's columns).
+__global__ void __launch_bounds__(1024) decode_band_merge_gather_kernel(
+    const unsigned* __restrict__ bkey, const int* __restrict__ bidx, int C, int S, int K, int H,
+    int W, int apply_sigmoid, const float* __restrict__ off, const float* __restrict__ dir,
+    const float* __restrict__ z, const float* __restrict__ dim, float* __restrict__ dets) {
+  __shared__ unsigned skey[2][kMergeMax];
+  __shared__ int sidx[2][kMergeMax];  // class * 2^26 + index (index < 2^26 = the order within a key)
+  const int b = blockIdx.x;
+  const int SK = S * K, N = C * SK;
+  const int HW = H * W;
+  for (int t = threadIdx.x; t < N; t += blockDim.x) {
+    const unsigned k = bkey[(size_t)b * N + t];
+    const int ix = bidx[(size_t)b * N + t];
+    skey[0][t] = k;
+    sidx[0][t] = ix == 0x7fffffff ? 0x7fffffff : (t / SK) * (1 << 26) + ix;
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int nl = C * S; nl > 1; nl = (nl + 1) >> 1) {
+    const unsigned* ik = skey[cur];
+    const int* ii = sidx[cur];
+    unsigned* ok = skey[cur ^ 1];
+    int* oi = sidx[cur ^ 1];
+    for (int t = threadIdx.x; t < nl * K; t += blockDim.x) {
+      const int l = t / K, p = t - l * K;
+      const unsigned k = ik[t];
+      const int ci = ii[t];
+      int rank = p;
+      if (!((nl & 1) && l == nl - 1)) {  // the odd list out is carried over as it is
+        const bool left = (l & 1) == 0;
+        const unsigned* pk = ik + (l ^ 1) * K;
+        const int* pi = ii + (l ^ 1) * K;
+        int lo = 0, hi = K;  // partner entries preceding (k, ci)
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          const unsigned km = pk[mid];
+          const int im = pi[mid];
+          const bool before = km > k || (km == k && (left ? im < ci : im <= ci));
+          if (before)
+            lo = mid + 1;
+          else
+            hi = mid;
+        }
+        rank += lo;
+      }
+      if (rank < K) {
+        ok[(l >> 1) * K + rank] = k;
+        oi[(l >> 1) * K + rank] = ci;
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  for (int rank = threadIdx.x; rank < K; rank += blockDim.x) {
+    const unsigned k = skey[cur][rank];
+    const int ci = sidx[cur][rank];
+    const int cls = ci >> 26;
+    const int ind = ci & ((1 << 26) - 1);
+    if (ci == 0x7fffffff || ind >= HW || cls >= C) {  // a sentinel: unreachable while K <= H*W
+      float* d = dets + ((size_t)b * K + rank) * 10;  // (sfa_decode checks it); never gathered
+      for (int q = 0; q < 10; ++q) d[q] = 0.f;
+      continue;
+    }
+    float xs = (float)(ind % W);
+    float ys = (float)(ind / W);
+    if (off) {
+      float o0 = off[((size_t)b * 2 + 0) * HW + ind];
+      float o1 = off[((size_t)b * 2 + 1) * HW + ind];
+      if (apply_sigmoid) {
+        o0 = sigmoid_clamp_f(o0);
+        o1 = sigmoid_clamp_f(o1);
+      }
+      xs = xs + o0;
+      ys = ys + o1;
+    } else {
+      xs = xs + 0.5f;
+      ys = ys + 0.5f;
+    }
+    float* d = dets + ((size_t)b * K + rank) * 10;
+    d[0] = fkey_inv(k);
+    d[1] = xs;
+    d[2] = ys;
+    d[3] = z[(size_t)b * HW + ind];
+    d[4] = dim[((size_t)b * 3 + 0) * HW + ind];
+    d[5] = dim[((size_t)b * 3 + 1) * HW + ind];
+    d[6] = dim[((size_t)b * 3 + 2) * HW + ind];
+    d[7] = dir[((size_t)b * 2 + 0) * HW + ind];
+    d[8] = dir[((size_t)b * 2 + 1) * HW + ind];
+    d[9] = (float)cls;
+  }
+}
+
+// Band geometry: S bands of R rows (8 preferred: 384 workgroups at B = 16, C = 3) with
+// C * S * K <= kMergeMax, (R + 2) * (W + 2) <= kBandMaxTile and ceil(R * W / 512) <= kBandMaxIPT;
+// S = 0 when no band split fits (one block per class, the kernels above).
+static void band_plan(int C, int H, int W, int K, int* S_out, int* R_out) {
+  *S_out = 0;
+  *R_out = H;
+  static const int order[] = {8, 9, 10, 11, 12, 13, 14, 15, 16, 7, 6, 5, 4, 3, 2, 1};
+  for (int S : order) {
+    if (S > H) continue;
+    const int R = (H + S - 1) / S;
+    const int S_eff = (H + R - 1) / R;
+    if (C * S_eff * K > kMergeMax) continue;
+    if ((R + 2) * (W + 2) > kBandMaxTile || (R + 2) * (W + 2) > kBandMaxLoads * kBandThreads) continue;
+    if ((R * W + kBandThreads - 1) / kBandThreads > kBandMaxIPT) continue;
+    *S_out = S_eff;
+    *R_out = R;
+    return;
+  }
+}
+
 }  // namespace sfa
 
 using namespace sfa;
 
 extern "C" size_t sfa_decode_workspace_size(int batch, int num_classes, int K) {
   if (batch <= 0 || num_classes <= 0 || K <= 0) return 0;
-  const size_t n = (size_t)batch * num_classes * K;
+  // the band candidates (C * S * K per frame, S <= 16) or the per-class ones (C * K)
+  const size_t n = (size_t)batch * num_classes * K * 16;
   return align_up(n * sizeof(unsigned), 256) + align_up(n * sizeof(int), 256);
 }
 
@@ -295,6 +639,24 @@ extern "C" int sfa_decode(const float* hm, const float* off, const float* dir, c
     return SFA_E_WORKSPACE;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  int S = 0, R = height;
+  band_plan(num_classes, height, width, K, &S, &R);
+  if (S > 0) {
+    const size_t nb = (size_t)batch * num_classes * S * K;
+    auto* bk = reinterpret_cast<unsigned*>(workspace);
+    auto* bi = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + align_up(nb * sizeof(unsigned), 256));
+    if (align_up(nb * sizeof(unsigned), 256) + nb * sizeof(int) > workspace_bytes) {
+      set_error("decode: workspace too small");
+      return SFA_E_WORKSPACE;
+    }
+    hipLaunchKernelGGL(decode_band_topk_kernel<0>, dim3(S, num_classes, batch), dim3(kBandThreads), 0, st, hm,
+                       num_classes, height, width, K, R, apply_sigmoid, bk, bi);
+    SFA_LAUNCH_CHECK();
+    hipLaunchKernelGGL(decode_band_merge_gather_kernel, dim3(batch), dim3(1024), 0, st, bk, bi, num_classes, S,
+                       K, height, width, apply_sigmoid, off, dir, z, dim, dets);
+    SFA_LAUNCH_CHECK();
+    return SFA_OK;
+  }
   const size_t n = (size_t)batch * num_classes * K;
   auto* ck = reinterpret_cast<unsigned*>(workspace);
   auto* ci = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) +

@@ -748,27 +748,34 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.part_floats = bf.part_floats;
   };
 
+  const int H2 = H / 2, W2 = W / 2;
+  const bool pool_fused = h3 && m->pool_fusion && H2 % 8 == 0 && W2 % 16 == 0;
+  // The patch stem reads the caller's layout itself and scales every tile by its own max |x|:
+  // no layout conversion, no input amax pass (stem_patch_kernel.h).
+  const bool patch_stem = pool_fused && m->stem_patch && H2 % 16 == 0 && W2 % 16 == 0;
   const float* xin = x;
-  if (in_layout != SFA_IN_NHWC4) {
+  if (patch_stem) {
+  } else if (in_layout != SFA_IN_NHWC4) {
     SFA_RC(launch_nchw3_to_nhwc4(x, F(bf.xin), B, H, W, in_layout == SFA_IN_NCHW3_FLIP_HW,
                                  AM(AM_INPUT), st));
     xin = F(bf.xin);
   } else if (h3) {
     SFA_RC(launch_amax_nhwc4(x, B, H, W, AM(AM_INPUT), st));
   }
-  const int H2 = H / 2, W2 = W / 2;
   // stem conv7x7/s2/p3 + BN + ReLU   (fpn_resnet.py:179-181)
   // fp16x3 with an 8x16-tileable stem output: the max-pool (:182) runs in the stem's epilogue.
   // Patch stem (default): every pooled cell has one owner tile, the neighbours' parts of the
   // tile-border cells go through a side buffer and a merge pass (no memset, no atomics).
   // Implicit-GEMM stem (SFA_STEM_PATCH=0) and the patch stem's A/B form
   // (SFA_STEM_PATCH_ATOMIC=1): pooled buffer zeroed, border cells combined with atomicMax.
-  const bool pool_fused = h3 && m->pool_fusion && H2 % 8 == 0 && W2 % 16 == 0;
   {
     ConvArgs a = conv_args(wb, p.stem, B, H2, W2, pool_fused ? F(bf.p0) : F(bf.s0), nullptr, 1);
-    a.seg[0] = seg(xin, B, H, W, 4, 7, 2, 3);
+    a.seg[0] = seg(xin, B, H, W, 4, 7, 2, 3);  // the patch stem reads NCHW3 planes through it too
     io(a, AM_INPUT, -1, AM_STEM);
-    if (pool_fused && m->stem_patch && H2 % 16 == 0 && W2 % 16 == 0) {
+    if (patch_stem) {
+      a.amax_in[0] = nullptr;  // per-tile scales
+      a.stem_in = in_layout == SFA_IN_NHWC4 ? STEM_IN_NHWC4
+                                             : (in_layout == SFA_IN_NCHW3_FLIP_HW ? STEM_IN_NCHW3_FLIP : STEM_IN_NCHW3);
       if (m->stem_atomic) {
         a.part = nullptr;
         a.part_floats = 0;

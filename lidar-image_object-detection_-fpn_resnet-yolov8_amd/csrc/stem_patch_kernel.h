@@ -11,6 +11,15 @@
 // stay in LDS for the block's lifetime; blocks loop over tiles (grid = CUs) and prefetch
 // the next tile's patch into registers while the current tile computes. Epilogue: the
 // stem + pool epilogue of conv_h3_kernel (h3_pool_epilogue, 16 x 16 tiles).
+//
+// Round 3: the patch is read straight from the caller's layout (IN: NHWC4 from the voxeliser,
+// or the reference's NCHW3 planes, optionally flipped for the back view), and each tile scales
+// its patch by a power of two from ITS OWN max |x| (reduced over the prefetched patch while the
+// previous tile computes) instead of the frame's: the layout-conversion pass (a 71 MB read +
+// 95 MB write per 16 frames) and the input amax pass are gone.  A power-of-two scale only moves
+// the fp16 terms' exponents, so products, f32 sums and the 1/s rescale give the same bits as
+// the frame scale whenever the lo terms stay normal fp16 (|x| > 2^-16 of the scale's max; a
+// tile's max is <= its frame's, so the tile scale is the more accurate one below that).
 #pragma once
 
 #include "conv_h3_kernel.h"
@@ -28,7 +37,8 @@ constexpr int PATCH_TERM = PIX * 8;            // 4 fp16 per pixel
 constexpr int NT = 512, NW = 8;
 constexpr int PF = (PIX + NT - 1) / NT;        // patch pixels prefetched per thread (3)
 constexpr int T_BYTES = 256 * (64 + 4) * 4 + 2 * NW * 4;  // h3_pool_epilogue's LDS
-constexpr int LDS_BYTES = W_BYTES + 2 * PATCH_TERM + T_BYTES;  // 151,600 B: one block per CU
+constexpr int WM_BYTES = NW * 4;                             // per-wave max |x| of the next patch
+constexpr int LDS_BYTES = W_BYTES + 2 * PATCH_TERM + T_BYTES + WM_BYTES;  // 151,632 B: one block per CU
 }  // namespace stem_patch
 
 // Epilogue for one 16 x 16 tile (th, tw) of frame b: ReLU(conv * 1/s * winv + b) into LDS,
@@ -179,7 +189,7 @@ __global__ void __launch_bounds__(256) stem_pool_merge_kernel(const ConvArgs a, 
 // 4 = no patch fetch, 8 = first patch fetched after the weights are staged,
 // 16 = border cells stored instead of atomicMax (only with a.part == null: the atomic A/B form),
 // 64 = the 32x32x16 MFMA form (round 1) instead of 16x16x32 (same products, other summation order)
-template <int ABL = 0>
+template <int ABL = 0, int IN = STEM_IN_NHWC4>
 __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs a, int ntiles) {
   using namespace stem_patch;
   constexpr bool M16 = (ABL & 64) == 0;  // 16x16x32 MFMAs (default); ABL 64: the 32x32x16 form
@@ -188,6 +198,7 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs 
   unsigned char* SU = smem + W_BYTES;                   // patch, 2 terms
   unsigned char* ST = smem + W_BYTES + 2 * PATCH_TERM;  // epilogue tile (its own LDS: no barrier
                                                         // between a tile's epilogue and the next patch)
+  float* WM = reinterpret_cast<float*>(smem + W_BYTES + 2 * PATCH_TERM + T_BYTES);
   // LDS-only barrier (the no-return pooled atomics of the previous tile stay in flight)
   auto lds_barrier = [] {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -198,23 +209,46 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tw_n = a.OW / TW, tiles_per_frame = (a.OH / TH) * tw_n;
 
-  x6_f32x4 pf[PF];
-  auto fetch = [&](int tile) {
+  // two patch prefetch sets: tile t's patch is loaded two tiles ahead (set t & 1), so the loads
+  // have a whole tile (MFMAs + epilogue) to land before its max and split are needed
+  x6_f32x4 pf0[PF], pf1[PF];
+  auto fetch = [&](int tile, x6_f32x4 (&pf)[PF]) {
     const int b = tile / tiles_per_frame, tl = tile - b * tiles_per_frame;
     const int th = tl / tw_n, tw = tl - th * tw_n;
     const int iy0 = 2 * TH * th - 3, ix0 = 2 * TW * tw - 3;
-    const x6_f32x4* x = reinterpret_cast<const x6_f32x4*>(g.x) + (size_t)b * g.H * g.W;
+    const size_t hw = (size_t)g.H * g.W;
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       const int p = tid + j * NT;
       const int py = p / PW, px = p - py * PW;
       const int iy = iy0 + py, ix = ix0 + px;
       x6_f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (p < PIX && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W) v = x[iy * g.W + ix];
+      if (p < PIX && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W) {
+        if constexpr (IN == STEM_IN_NHWC4) {
+          v = reinterpret_cast<const x6_f32x4*>(g.x)[(size_t)b * hw + iy * g.W + ix];
+        } else {  // the reference's (B, 3, H, W) planes; channel 3 of the patch pixel stays 0
+          const int sy = IN == STEM_IN_NCHW3_FLIP ? g.H - 1 - iy : iy;
+          const int sx = IN == STEM_IN_NCHW3_FLIP ? g.W - 1 - ix : ix;
+          const float* x = g.x + (size_t)b * 3 * hw + (size_t)sy * g.W + sx;
+          v[0] = x[0];
+          v[1] = x[hw];
+          v[2] = x[2 * hw];
+        }
+      }
       pf[j] = v;
     }
   };
-  auto store_patch = [&](float s) {
+  // max |x| of the prefetched patch: this wave's part into WM (read after the next barrier)
+  auto patch_max_to_lds = [&](const x6_f32x4 (&pf)[PF]) {
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(pf[j][0]), fabsf(pf[j][1])), fmaxf(fabsf(pf[j][2]), fabsf(pf[j][3]))));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (lane == 0) WM[wave] = m;
+  };
+  auto store_patch = [&](float s, const x6_f32x4 (&pf)[PF]) {
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       const int p = tid + j * NT;
@@ -234,8 +268,12 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs 
   const int abase = ((2 * oyl) * PW + 2 * oxl + 2 * h) * 8;
   const int bbase = r * WROW + 16 * h;
 
+  const int G = gridDim.x;
   int tile = blockIdx.x;
-  if (tile < ntiles && !(ABL & 4) && !(ABL & 8)) fetch(tile);  // in flight while the weights are staged
+  if (!(ABL & 4) && !(ABL & 8)) {  // in flight while the weights are staged
+    if (tile < ntiles) fetch(tile, pf0);
+    if (tile + G < ntiles) fetch(tile + G, pf1);
+  }
   // weights: wh [2][64][Kpad] with k = (kh 7 + kw) 4 + c  ->  LDS [2][64][WROW] at k' = (kh 8 + kw) 4 + c
 #pragma unroll
   for (int i = tid; i < 2 * 64 * 56; i += NT) {
@@ -248,16 +286,28 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs 
     *reinterpret_cast<uint2*>(SW + t * 64 * WROW + n * WROW + tap * 8) = v;
   }
 
-  if (tile < ntiles && !(ABL & 4) && (ABL & 8)) fetch(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
+  if (!(ABL & 4) && (ABL & 8)) {
+    if (tile < ntiles) fetch(tile, pf0);
+    if (tile + G < ntiles) fetch(tile + G, pf1);
+  }
+  if (tile < ntiles) patch_max_to_lds(pf0);
+  // one tile: patch `cur` (its max already in WM) split into LDS, the tile two ahead fetched into
+  // `cur`, MFMAs, epilogue, then the max of `nxt` (the next tile's patch) into WM
+  auto body = [&](int tile, x6_f32x4 (&cur)[PF], x6_f32x4 (&nxt)[PF]) {
+    // WM of this patch visible (written after the previous tile's epilogue); first time round
+    // also the staged weights
+    __syncthreads();
     const int b = tile / tiles_per_frame;
     float ainv[1];
-    const float as = amax_frame_scale(a.amax_in, 1, b, ainv[0]);
-    store_patch(as);
+    float tmax = WM[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) tmax = fmaxf(tmax, WM[w]);
+    const float as = amax_scale_bits(__float_as_uint(tmax), ainv[0]);
+    store_patch(as, cur);
     // patch (and, first time round, the weights) in LDS; every wave is past the previous
     // tile's epilogue reads of ST
     lds_barrier();
-    if (tile + (int)gridDim.x < ntiles && !(ABL & 4)) fetch(tile + gridDim.x);  // lands during the MFMAs
+    if (tile + 2 * G < ntiles && !(ABL & 4)) fetch(tile + 2 * G, cur);  // lands during the next tile
 
     float mx;
     if constexpr (M16) {
@@ -331,11 +381,22 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs 
       const int tl = tile - b * tiles_per_frame, th = tl / tw_n;
       stem_pool_epilogue<(ABL & 16) != 0>(a, mx, reinterpret_cast<float*>(ST), b, th, tl - th * tw_n, tid);
     }
+    // the next patch's max into WM (every wave read WM before this tile's lds_barrier)
+    if (tile + G < ntiles) patch_max_to_lds(nxt);
+  };
+  for (;;) {
+    if (tile >= ntiles) break;
+    body(tile, pf0, pf1);
+    tile += G;
+    if (tile >= ntiles) break;
+    body(tile, pf1, pf0);
+    tile += G;
   }
 }
 
 // Grid = one block per CU (each loops over tiles); needs the stem's fp16x3 split weights
-// (Kpad >= 196), NHWC4 input, conv output divisible into 16 x 16 tiles.
+// (Kpad >= 196), the input as a.stem_in says (seg 0 describes it as 4 channels), conv output
+// divisible into 16 x 16 tiles.
 inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
   const ConvSeg& g = a.seg[0];
   if (!a.wh || !a.winv || a.nseg != 1 || a.N != 64 || g.C != 4 || g.KH != 7 || g.KW != 7 || g.stride != 2 ||
@@ -357,15 +418,27 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
   if (grid <= 0) return SFA_OK;
   const int abl = a.stem_abl;  // SFA_OPT_STEM_ABL of the model (timing ablations only)
   const dim3 gd((unsigned)grid), bd(stem_patch::NT);
+  constexpr int NC3 = STEM_IN_NCHW3;  // ablations: the bench's input layout
+  if (abl != 0 && a.stem_in != NC3) {
+    set_error("stem_patch: ablations are built for the NCHW3 input only");
+    return SFA_E_UNSUPPORTED;
+  }
   switch (abl) {
-    case 1: hipLaunchKernelGGL(stem_patch_pool_kernel<1>, gd, bd, 0, st, a, ntiles); break;
-    case 2: hipLaunchKernelGGL(stem_patch_pool_kernel<2>, gd, bd, 0, st, a, ntiles); break;
-    case 4: hipLaunchKernelGGL(stem_patch_pool_kernel<4>, gd, bd, 0, st, a, ntiles); break;
-    case 3: hipLaunchKernelGGL(stem_patch_pool_kernel<3>, gd, bd, 0, st, a, ntiles); break;
-    case 8: hipLaunchKernelGGL(stem_patch_pool_kernel<8>, gd, bd, 0, st, a, ntiles); break;
-    case 16: hipLaunchKernelGGL(stem_patch_pool_kernel<16>, gd, bd, 0, st, a, ntiles); break;
-    case 64: hipLaunchKernelGGL(stem_patch_pool_kernel<64>, gd, bd, 0, st, a, ntiles); break;
-    default: hipLaunchKernelGGL(stem_patch_pool_kernel<0>, gd, bd, 0, st, a, ntiles); break;
+    case 1: hipLaunchKernelGGL((stem_patch_pool_kernel<1, NC3>), gd, bd, 0, st, a, ntiles); break;
+    case 2: hipLaunchKernelGGL((stem_patch_pool_kernel<2, NC3>), gd, bd, 0, st, a, ntiles); break;
+    case 4: hipLaunchKernelGGL((stem_patch_pool_kernel<4, NC3>), gd, bd, 0, st, a, ntiles); break;
+    case 3: hipLaunchKernelGGL((stem_patch_pool_kernel<3, NC3>), gd, bd, 0, st, a, ntiles); break;
+    case 8: hipLaunchKernelGGL((stem_patch_pool_kernel<8, NC3>), gd, bd, 0, st, a, ntiles); break;
+    case 16: hipLaunchKernelGGL((stem_patch_pool_kernel<16, NC3>), gd, bd, 0, st, a, ntiles); break;
+    case 64: hipLaunchKernelGGL((stem_patch_pool_kernel<64, NC3>), gd, bd, 0, st, a, ntiles); break;
+    default:
+      switch (a.stem_in) {
+        case STEM_IN_NCHW3: hipLaunchKernelGGL((stem_patch_pool_kernel<0, STEM_IN_NCHW3>), gd, bd, 0, st, a, ntiles); break;
+        case STEM_IN_NCHW3_FLIP:
+          hipLaunchKernelGGL((stem_patch_pool_kernel<0, STEM_IN_NCHW3_FLIP>), gd, bd, 0, st, a, ntiles);
+          break;
+        default: hipLaunchKernelGGL((stem_patch_pool_kernel<0, STEM_IN_NHWC4>), gd, bd, 0, st, a, ntiles); break;
+      }
   }
   SFA_LAUNCH_CHECK();
   if (a.part) {

@@ -114,3 +114,29 @@ def test_decode_without_offset(gpu):
     got = runtime.decode(_t(hm, gpu), None, _t(o["dir"], gpu), _t(o["z"], gpu), _t(o["dim"], gpu),
                          K=50).cpu().numpy()
     np.testing.assert_array_equal(got, decode_oracle.decode(hm, None, o["dir"], o["z"], o["dim"], K=50))
+
+
+@pytest.mark.parametrize("B,C,H,W,K", [
+    (3, 3, 37, 29, 50),      # odd bands (R = 5: 8 bands, last one 2 rows), halo rows at every cut
+    (2, 3, 10, 10, 50),      # K > band pixels: per-band lists padded with sentinels
+    (1, 1, 152, 152, 256),   # C * S * K limit: fewer bands
+    (2, 16, 24, 24, 256),    # C * K = 4096: one band per class
+    (1, 3, 3, 4100, 40),     # a band tile wider than LDS allows: the one-block-per-class kernels
+    (2, 3, 152, 152, 50),    # production shape with quantised values: ties across band cuts
+])
+def test_decode_band_split_shapes(gpu, B, C, H, W, K):
+    """The band-parallel decode (S row bands per class map, sorted band lists merged per frame)
+    == the oracle's two topk stages bit for bit, on shapes that stress every band edge: odd
+    heights, lists shorter than K, the C*S*K cap, the fallback kernels, plateaus and equal
+    values crossing band cuts (quantised maps: many ties, ordered by lower index, then class)."""
+    rng = np.random.default_rng(B * 1000 + H + W + K)
+    hm = rng.random((B, C, H, W), dtype=np.float32)
+    if (H, W) == (152, 152) and K == 50:
+        hm = (np.floor(hm * 64) / 64).astype(np.float32)  # heavy ties, plateaus across cuts
+        hm[:, :, 17:23, :] = np.float32(1.0)               # a 6-row plateau over the cut at row 19
+    maps = {k: rng.standard_normal((B, c, H, W)).astype(np.float32)
+            for k, c in (("off", 2), ("dir", 2), ("z", 1), ("dim", 3))}
+    got = runtime.decode(_t(hm, gpu), *(_t(maps[k], gpu) for k in ("off", "dir", "z", "dim")),
+                         K=K).cpu().numpy()
+    exp = decode_oracle.decode(hm, maps["off"], maps["dir"], maps["z"], maps["dim"], K=K)
+    np.testing.assert_array_equal(got, exp)
