@@ -191,6 +191,10 @@ struct ConvArgs {
   // SFA_OPT_STEM_ABL (timing ablations of the patch stem; wrong results by design).
   int tune;
   int stem_abl;
+  // Split-K tickets (model workspace, zero between launches; 2 words per output tile): when set,
+  // split-K launches combine their slices in the kernel (the last slice to arrive adds the others'
+  // partials in slice order and runs the epilogue) instead of a separate reduce launch.
+  unsigned* tile_cnt;
   // Patch stem input (stem_patch_kernel.h): STEM_IN_NHWC4 (the voxeliser's layout), STEM_IN_NCHW3
   // (the reference's (B, 3, H, W)), STEM_IN_NCHW3_FLIP (read as torch.flip(x, [2, 3])); every
   // 16 x 16 output tile scales its fp16x3 patch by its own max |x| (no layout / amax pass).

@@ -40,6 +40,47 @@ static int launch_conv_x6(const ConvArgs& a, int epilogue, hipStream_t st) {
   return rc;
 }
 
+static int num_cus() {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0, n = 0;
+    ncu = (hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
+              ? n
+              : 256;
+  }
+  return ncu;
+}
+
+// Split-K slices of a 128 x 128-tiled body conv (fp16x3, standard epilogue with bias).
+// Default (round 2's rule): 2 slices for the 512-wide convs, combined by splitk_reduce_kernel.
+// OPT_CONV_TUNE bit 1024 (experimental, measured slower: model.hip tuned()) combines the slices
+// in the kernel (a.tile_cnt: the last slice adds the others' partials) and balances the grid —
+// 2 blocks per CU run at once and a block's time is set by its K steps, so the count minimises
+// ceil(tiles * ks / slots) / ks (+ 5 % of a block per extra slice) over the divisors of the
+// conv's K steps; bits 12..15 force a count. Tiles are priced at 16 frames of the conv's
+// geometry, so a frame's arithmetic never depends on its batch.
+static int pick_ksplit(const ConvArgs& a, int ksteps, bool inkernel) {
+  if (!a.part || !a.bias || a.wstride || a.wk0 || a.res_up) return 1;
+  const int forced = (a.tune >> 12) & 15;
+  if (forced) return ksteps % forced == 0 ? forced : 1;
+  if (!(a.tune & 1024) || !inkernel || !a.tile_cnt) return a.N >= 512 ? 2 : 1;
+  const long long tiles = (tile_rows(a) + 127) / 128 * (a.N / 128);
+  const long long slots = 2LL * num_cus();
+  int best = 1;
+  double best_cost = 1e30;
+  for (int ks = 1; ks <= 8; ++ks) {
+    if (ksteps % ks) continue;
+    const double rounds = (double)((tiles * ks + slots - 1) / slots);
+    const double cost = rounds / ks + 0.05 * (ks - 1);
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = ks;
+    }
+  }
+  return best;
+}
+
 // One-segment 3x3 / stride 1 / pad 1 conv with 32-channel chunks: conv_h3s_kernel applies.
 static bool strip_ok(const ConvArgs& a) {
   const ConvSeg& g = a.seg[0];
@@ -134,7 +175,11 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   }
   if (a.N % 128 == 0) {
     ConvArgs b = a;
-    b.ksplit = a.part && a.N >= 512 && !sliced && a.bias ? 2 : 1;
+    const bool r3_big = !strip && tile_rows(a) >= 50000 && !(a.tune & 8);  // conv_r3 below: in-kernel split
+    if (strip)
+      b.ksplit = pick_ksplit(a, 3 * (a.seg[0].C >> 5), !(a.tune & 16) && !(a.tune & 2));
+    else
+      b.ksplit = pick_ksplit(a, a.Kpad / 32, r3_big);
     if (strip) {
       if (a.tune & 16)
         rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);

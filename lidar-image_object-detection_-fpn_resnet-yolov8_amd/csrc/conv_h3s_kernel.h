@@ -370,6 +370,10 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (nsplit > 1 && (ABL & 2) != 0 && a.tile_cnt) {  // in-kernel split-K (conv_r3_kernel.h)
+    r3t_splitk_combine<TM, TN, NT>(a, acc, smem, lbid, kz, nsplit, m0 + wave * WM, m0, n0, lane, ainv);
+    return;
+  }
   if (nsplit > 1 && (ABL & 2) != 0) {  // split-K partials, transposed form: float4 per lane
     float* part = a.part + (size_t)kz * M * a.N;
 #pragma unroll
@@ -442,7 +446,7 @@ inline int launch_conv_h3s_cfg(const ConvArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((conv_h3s_kernel<BM, BN, WM, EPI, OCC, ABL>), dim3((unsigned)nblocks), dim3((BM / WM) * 64), 0,
                      st, a);
   SFA_LAUNCH_CHECK();
-  if (ks > 1) {
+  if (ks > 1 && !((ABL & 2) != 0 && a.tile_cnt)) {  // no in-kernel combine: the reduce launch
     const long long nel = (long long)a.M * a.N;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((nel + 1023) / 1024)), dim3(256), 0, st, a);
     SFA_LAUNCH_CHECK();

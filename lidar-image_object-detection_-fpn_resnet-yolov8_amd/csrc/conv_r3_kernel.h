@@ -163,6 +163,86 @@ __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&ac
                                reinterpret_cast<float*>(smem + (STG ? (NT / 64) * (TM * 16) * PITCH : 0)));
 }
 
+// In-kernel split-K (a.tile_cnt, transposed accumulators). Slice tickets are drawn in arrival
+// order: the first nsplit - 1 arrivals write their partial (acc * ainv * winv, as for the reduce
+// launch) into part[kz] and publish it; the last arrival waits for those nsplit - 1 publications
+// (they are running: they drew their tickets before it) and combines, for each of its float4s,
+// part[0] + part[1] + ... in SLICE order — its own slice from registers — then + bias, + residual,
+// ReLU, exactly as splitk_reduce_kernel does (same bits), stores y and records the frame maxima.
+// The last block also resets the tile's two words (zero for the next launch). Returns true if the
+// block is done (it wrote a partial, or combined), i.e. always; the caller returns.
+template <int TM, int TN, int NT>
+__device__ __forceinline__ void r3t_splitk_combine(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
+                                                   int tile, int kz, int nsplit, int mrow0, int m0, int n0, int lane,
+                                                   const float (&ainv)[TM]) {
+#pragma clang fp contract(off)
+  const int M = a.M, c16 = lane & 15, g = lane >> 4;
+  int* flag = reinterpret_cast<int*>(smem);
+  unsigned* tk = a.tile_cnt + 2 * tile;
+  __syncthreads();  // every wave is past its last LDS read of the K loop: smem is free
+  if (threadIdx.x == 0) *flag = (int)atomicAdd(tk, 1u);
+  __syncthreads();
+  const bool last = *flag == nsplit - 1;
+  if (!last) {
+    float* part = a.part + (size_t)kz * M * a.N;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int m = mrow0 + mi * 16 + c16, n = n0 + ni * 16 + 4 * g;
+        const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(a.winv + n);
+        x6_f32x4 val;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) val[v] = acc[mi][ni][v] * ainv[mi] * cs[v];
+        if (m < M) *reinterpret_cast<x6_f32x4*>(part + (size_t)m * a.N + n) = val;
+      }
+    __threadfence();  // this thread's partial is device-visible ...
+    __syncthreads();  // ... and every thread's, before the publication
+    if (threadIdx.x == 0) atomicAdd(tk + 1, 1u);
+    return;
+  }
+  if (threadIdx.x == 0) {
+    // the other slices hold tickets, so they are resident and finish their partial without
+    // waiting on anything: the wait is bounded (the cap only guards a broken launch)
+    for (int it = 0; it < (1 << 22); ++it) {
+      if (__hip_atomic_load(tk + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nsplit - 1)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    tk[0] = 0u;
+    tk[1] = 0u;
+  }
+  __syncthreads();
+  __threadfence();  // acquire: the other slices' partials
+  AmaxRows am(a.OH * a.OW, m0);
+#pragma unroll
+  for (int ni = 0; ni < TN; ++ni) {
+    const int n = n0 + ni * 16 + 4 * g;
+    const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(a.winv + n);
+    const x6_f32x4 bn = *reinterpret_cast<const x6_f32x4*>(a.bias + n);
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = mrow0 + mi * 16 + c16;
+      if (m >= M) continue;
+      x6_f32x4 own;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) own[v] = acc[mi][ni][v] * ainv[mi] * cs[v];
+      const size_t e = (size_t)m * a.N + n;
+      x6_f32x4 sum = kz == 0 ? own : *reinterpret_cast<const x6_f32x4*>(a.part + e);
+      for (int z = 1; z < nsplit; ++z)
+        sum += z == kz ? own : *reinterpret_cast<const x6_f32x4*>(a.part + (size_t)z * M * a.N + e);
+      sum += bn;
+      if (a.res) sum += *reinterpret_cast<const x6_f32x4*>(a.res + e);
+      if (a.relu) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) sum[v] = fmaxf(sum[v], 0.f);
+      }
+      *reinterpret_cast<x6_f32x4*>(a.y + e) = sum;
+      if (a.amax_out) am.add(a.amax_out, m, fmaxf(fmaxf(fabsf(sum[0]), fabsf(sum[1])), fmaxf(fabsf(sum[2]), fabsf(sum[3]))));
+    }
+  }
+  if (a.amax_out) amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1, reinterpret_cast<float*>(smem + 16));
+}
+
 // Heads (EPI_HEAD, transposed form): per head and pixel, ReLU(conv3x3 + b) of the lane's 16 of
 // the head's 64 channels and the 1x1 conv's partial sums over them (4 outputs x TM pixels),
 // reduced over the pixel's four lanes (l, l ^ 16, l ^ 32, l ^ 48) by v_permlane32/16_swap: each
@@ -664,6 +744,10 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   float ainv[TM];
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi) ainv[mi] = 1.f / as[mi];
+  if (nsplit > 1 && (ABL & 2048) != 0 && a.tile_cnt && EPI == EPI_STD) {  // in-kernel split-K
+    r3t_splitk_combine<TM, TN, NT>(a, acc, smem, lbid, kz, nsplit, m0 + wave * WM, m0, n0, lane, ainv);
+    return;
+  }
   if (nsplit > 1 && (ABL & 2048) != 0) {  // split-K partials, transposed form: float4 per lane
     float* part = a.part + (size_t)kz * M * a.N;
 #pragma unroll
@@ -763,7 +847,7 @@ inline int launch_conv_r3_cfg(const ConvArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((conv_r3_kernel<BM, BN, WM, EPI, OCC, NSTAGE, 1, ABL>), dim3((unsigned)nblocks),
                        dim3((BM / WM) * 64), 0, st, a);
   SFA_LAUNCH_CHECK();
-  if (ks > 1) {
+  if (ks > 1 && !((ABL & 2048) != 0 && a.tile_cnt)) {  // no in-kernel combine: the reduce launch
     const long long nel = (long long)a.M * a.N;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((nel + 1023) / 1024)), dim3(256), 0, st, a);
     SFA_LAUNCH_CHECK();

@@ -316,6 +316,10 @@ struct sfa_model {
 static inline ConvArgs tuned(ConvArgs a, const sfa_model* m) {
   a.tune = m->tune;
   a.stem_abl = m->stem_abl;
+  // in-kernel split-K combining only on request (OPT_CONV_TUNE bit 1024): measured 35 % slower
+  // per forward than the reduce launch (profiles/r03e_ab_splitk_inkernel.txt) — the agent-scope
+  // fences a slice needs to publish its partial to another XCD write back / invalidate the L2
+  if (!(m->tune & 1024)) a.tile_cnt = nullptr;
   return a;
 }
 
@@ -603,8 +607,8 @@ namespace sfa {
 
 // Activation buffers of one forward (NHWC f32), carved from the workspace.
 struct Bufs {
-  size_t xin, s0, p0, t[4], a[4], l[4], up1, c1, up2, c2, up3, up4, L0, L1, L2, amax, part, part_floats,
-      total;
+  size_t xin, s0, p0, t[4], a[4], l[4], up1, c1, up2, c2, up3, up4, L0, L1, L2, amax, cnt, cnt_words, part,
+      part_floats, total;
 };
 
 // fp16x3 activation maxima (conv.h): per tensor a conv reads (named by its producer), B
@@ -644,9 +648,15 @@ static Bufs plan_bufs(const sfa_arch* arch, int B, int H, int W) {
   b.L0 = take((size_t)nch * B * P8);
   b.L1 = take((size_t)nch * B * P4);
   b.L2 = take((size_t)nch * B * P4);
-  b.amax = take((size_t)AM_COUNT * B * SFA_AMAX_WORDS);
-  // split-K partial sums of the widest convs (conv.hip: 2 slices at 512 channels; room for 4)
-  b.part_floats = (size_t)4 * B * (H / 32) * (W / 32) * 512;
+  // the activation maxima, then the split-K tile tickets (2 words per 128 x 128 output tile of
+  // the most-tiled split conv, layer2: B (H / 8) (W / 8) / 128 rows of tiles); zeroed together
+  // once per forward
+  b.cnt_words = 2 * ((size_t)B * (H / 32) * (W / 32) / 8 + 64);
+  b.amax = take((size_t)AM_COUNT * B * SFA_AMAX_WORDS + b.cnt_words);
+  b.cnt = b.amax + (size_t)AM_COUNT * B * SFA_AMAX_WORDS * 4;
+  // split-K partial sums (conv.hip pick_ksplit: up to 8 slices of layer4, 4 of layer3, 2 of layer2:
+  // 8 * B * (H / 32) * (W / 32) * 512 floats hold each of them)
+  b.part_floats = (size_t)8 * B * (H / 32) * (W / 32) * 512;
   b.part = take(b.part_floats);
   b.total = cur;
   return b;
@@ -739,13 +749,15 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     return h3 ? reinterpret_cast<unsigned*>(ws + bf.amax) + (size_t)slot * B * SFA_AMAX_WORDS : nullptr;
   };
   auto blk_slot = [](int li, int bi, int ci) { return AM_BLK + 4 * li + 2 * bi + ci; };
-  if (h3) SFA_HIP_TRY(hipMemsetAsync(ws + bf.amax, 0, (size_t)AM_COUNT * B * SFA_AMAX_WORDS * 4, st));
+  if (h3)
+    SFA_HIP_TRY(hipMemsetAsync(ws + bf.amax, 0, ((size_t)AM_COUNT * B * SFA_AMAX_WORDS + bf.cnt_words) * 4, st));
   auto io = [&](ConvArgs& a, int in0, int in1, int out) {
     a.amax_in[0] = in0 >= 0 ? AM(in0) : nullptr;
     a.amax_in[1] = in1 >= 0 ? AM(in1) : nullptr;
     a.amax_out = out >= 0 ? AM(out) : nullptr;
     a.part = F(bf.part);
     a.part_floats = bf.part_floats;
+    a.tile_cnt = h3 ? reinterpret_cast<unsigned*>(ws + bf.cnt) : nullptr;
   };
 
   const int H2 = H / 2, W2 = W / 2;

@@ -381,3 +381,33 @@ def test_stem_input_layouts_bit_exact(golden, gpu, hw):
     for h in gc.HEADS:
         r = ref[h].numpy()
         assert float(np.max(np.abs(a[h] - r) / np.maximum(1.0, np.abs(r)))) <= 1e-4, h
+
+
+def test_split_k_in_kernel_combine(golden, gpu):
+    """Experimental in-kernel split-K (OPT_CONV_TUNE bit 1024: the last slice to arrive adds the
+    others' partials in slice order) is bit-identical to the same split through the separate
+    reduce launch (the default), for forced 2- and 4-slice splits; its automatic split counts
+    (pick_ksplit) and no split agree to f32 rounding and with the reference."""
+    from oracle import model_oracle
+    x = torch.from_numpy(synthetic.synthetic_bev(3, 256, 320, seed=47)).to(gpu)
+
+    def run(tune):
+        model = make_model(golden, gpu)
+        eng = model._engine(gpu)
+        eng.set_math(_math("fp16x3"))
+        eng.set_option(_lib.OPT_CONV_TUNE, tune)
+        with torch.no_grad():
+            return {h: v.cpu().numpy() for h, v in model(x).items()}
+
+    for ks in (2, 4):
+        a, b = run((ks << 12) | 1024), run(ks << 12)
+        for h in gc.HEADS:
+            np.testing.assert_array_equal(a[h], b[h], err_msg=f"{h}: in-kernel vs reduce launch, {ks} slices")
+    auto, one = run(1024), run(1 << 12)
+    sd = gc.state_dict_np(golden.model)
+    ref = model_oracle.forward(model_oracle.state_dict_torch(sd), x.cpu(), dict(gc.HEADS))
+    for h in gc.HEADS:
+        r = ref[h].numpy()
+        scale = np.maximum(1.0, np.abs(r))
+        assert float(np.max(np.abs(auto[h] - one[h]) / scale)) <= 2e-5, h
+        assert float(np.max(np.abs(auto[h] - r) / scale)) <= 1e-4, h
