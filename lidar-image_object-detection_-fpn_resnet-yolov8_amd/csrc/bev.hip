@@ -17,6 +17,7 @@
 //     density = min(1, ln(count+1)/ln 64) (f64 table), written in the requested
 //     layout; the scratch cell is re-zeroed for the next call.
 // The result is independent of atomic arrival order: bit-exact.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -86,16 +87,16 @@ __global__ void __launch_bounds__(256) bev_scatter_kernel(const float4* __restri
 // One output cell: intensity = i[top], height = z'/4.0 (f32), density from the count (f64
 // table), stored in the requested layout (torch.flip(bev, [1, 2]) when FLIP).
 template <int LAYOUT, bool FLIP>
-__device__ __forceinline__ void bev_store_cell(const float4* __restrict__ pts, const BevArgs& a, int b, int cell,
-                                               unsigned cnt, unsigned long long key, void* __restrict__ out) {
-  float inten = 0.f, height = 0.f;
+__device__ __forceinline__ void bev_store_cell_i(const BevArgs& a, int b, int cell, unsigned cnt,
+                                                 unsigned long long key, float inten, void* __restrict__ out) {
+  float height = 0.f;
   double dens = 0.0;
   if (cnt) {
-    const unsigned idx = ~(unsigned)(key & 0xffffffffull);
     const float zr = __uint_as_float((unsigned)(key >> 32));
-    inten = pts[a.start[b] + idx].w;
     height = __fdiv_rn(zr, a.max_height);  // :43-44, f32 division
     dens = a.density[cnt < 63u ? cnt : 63u];
+  } else {
+    inten = 0.f;
   }
   // torch.flip(bev, [1, 2]): cell (r, c) lands at (607 - r, 607 - c)
   const int oc = FLIP ? kBevCells - 1 - cell : cell;
@@ -113,6 +114,18 @@ __device__ __forceinline__ void bev_store_cell(const float4* __restrict__ pts, c
     o[kBevCells] = (double)height;
     o[2 * kBevCells] = dens;
   }
+}
+
+// intensity = i of the cell's top point (the point index is the low word of the key)
+__device__ __forceinline__ float bev_top_intensity(const float4* __restrict__ pts, const BevArgs& a, int b,
+                                                   unsigned cnt, unsigned long long key) {
+  return cnt ? pts[a.start[b] + ~(unsigned)(key & 0xffffffffull)].w : 0.f;
+}
+
+template <int LAYOUT, bool FLIP>
+__device__ __forceinline__ void bev_store_cell(const float4* __restrict__ pts, const BevArgs& a, int b, int cell,
+                                               unsigned cnt, unsigned long long key, void* __restrict__ out) {
+  bev_store_cell_i<LAYOUT, FLIP>(a, b, cell, cnt, key, bev_top_intensity(pts, a, b, cnt, key), out);
 }
 
 template <int LAYOUT, bool FLIP>
@@ -147,8 +160,9 @@ __global__ void __launch_bounds__(256) bev_gather_kernel(const float4* __restric
 //   strip   per (frame, strip): ds_max_u64 / ds_add_u32 over its records in LDS (4,864
 //           cells: 58 KiB), then every cell of the strip written in the output layout.
 // The same keys and counts reach every cell (max and + are order-free): bit-identical to the
-// atomic path. Self-cleaning like it: the strip pass zeroes the records it read and its
-// strip's counters, so the scratch is zero again when the call's kernels have run.
+// atomic path. Self-cleaning like it: the strip pass zeroes its strip's counters. The records
+// have their own region after the atomic path's keys / counts (round 3: they used to overlap
+// them, so every record read was written back as zero — 16 B per point of extra traffic).
 constexpr int kStripRows = 8;
 constexpr int kStripCells = kStripRows * kBevW;   // 4,864
 constexpr int kStrips = kBevH / kStripRows;       // 76
@@ -272,7 +286,6 @@ __global__ void __launch_bounds__(kStripThreads) bev_strip_kernel(const float4* 
   const unsigned off = bs.offset[bin], cnt = bs.count[bin];
   for (unsigned r = threadIdx.x; r < cnt; r += kStripThreads) {
     const uint4 rec = bs.rec[off + r];
-    bs.rec[off + r] = make_uint4(0u, 0u, 0u, 0u);  // scratch zero again for the next call
     atomicMax(&skey[rec.z], ((unsigned long long)rec.y << 32) | rec.x);
     atomicAdd(&scnt[rec.z], 1u);
   }
@@ -286,14 +299,187 @@ __global__ void __launch_bounds__(kStripThreads) bev_strip_kernel(const float4* 
     bev_store_cell<LAYOUT, FLIP>(pts, a, b, strip * kStripCells + c, scnt[c], skey[c], out);
 }
 
+// ------------------------------------------------------- blocked-bin path --
+// Round 3 default: ONE pass over the points. Bin-pass block j of a frame takes its points
+// [1024 j, 1024 j + 1024) and writes their records into ITS OWN 1024-record region, grouped by
+// strip (LDS histogram, exclusive scan, LDS slot per point), plus one word per strip into a
+// table: (first record of the strip in the region) | (count << 16). The strip pass for
+// (frame, strip) walks the frame's table column and reduces those runs in LDS. No count pass,
+// no global scan, no global reservation atomics, and nothing to re-zero: the region and the
+// table are written before they are read. Region j of frame b starts at record
+// 1024 * (blk0[b] + j), blk0 = the exclusive sum of the frames' ceil(n / 1024) (host).
+constexpr int kBlkPts = 1024;
+constexpr int kBlkThreads = 256;
+constexpr int kBlkPPT = kBlkPts / kBlkThreads;  // 4
+
+struct BlkScratch {
+  uint4* rec;         // [total blocks][kBlkPts]
+  unsigned* tab;      // [total blocks][kStrips]: first | count << 16
+  int blk0[SFA_BEV_MAX_BATCH + 1];
+};
+
+template <bool RAW>
+__global__ void __launch_bounds__(kBlkThreads) bev_blk_bin_kernel(const float4* __restrict__ pts, BevArgs a,
+                                                                  BlkScratch bs) {
+  __shared__ unsigned hist[kStrips], first[kStrips];
+  const int b = blockIdx.y, j = blockIdx.x;
+  const int64_t s = a.start[b];
+  const int64_t n = a.start[b + 1] - s;
+  if ((int64_t)j * kBlkPts >= n) return;  // past this frame's points (the grid fits the largest)
+  for (int t = threadIdx.x; t < kStrips; t += kBlkThreads) hist[t] = 0u;
+  __syncthreads();
+  int cell[kBlkPPT], strip[kBlkPPT];
+  unsigned long long key[kBlkPPT];
+  unsigned slot[kBlkPPT];
+  float inten[kBlkPPT];
+  bool ok[kBlkPPT];
+#pragma unroll
+  for (int q = 0; q < kBlkPPT; ++q) {
+    const int64_t i = (int64_t)j * kBlkPts + q * kBlkThreads + threadIdx.x;
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < n) p = pts[s + i];
+    ok[q] = i < n && bev_point_cell<RAW>(p, a, i, cell[q], key[q]);
+    inten[q] = p.w;
+    strip[q] = ok[q] ? cell[q] / kStripCells : 0;
+    slot[q] = ok[q] ? atomicAdd(&hist[strip[q]], 1u) : 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {  // exclusive scan of the 76 strip counts (lane: bins 2 l, 2 l + 1)
+    const int l = threadIdx.x;
+    const unsigned c0 = 2 * l < kStrips ? hist[2 * l] : 0u, c1 = 2 * l + 1 < kStrips ? hist[2 * l + 1] : 0u;
+    unsigned x = c0 + c1;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned y = __shfl_up(x, d, 64);
+      if (l >= d) x += y;
+    }
+    const unsigned e0 = x - c0 - c1;
+    if (2 * l < kStrips) first[2 * l] = e0;
+    if (2 * l + 1 < kStrips) first[2 * l + 1] = e0 + c0;
+  }
+  __syncthreads();
+  const size_t region = (size_t)(bs.blk0[b] + j);
+  for (int t = threadIdx.x; t < kStrips; t += kBlkThreads) bs.tab[region * kStrips + t] = first[t] | (hist[t] << 16);
+  uint4* rec = bs.rec + region * kBlkPts;
+#pragma unroll
+  for (int q = 0; q < kBlkPPT; ++q)
+    if (ok[q])
+      rec[first[strip[q]] + slot[q]] = make_uint4((unsigned)(key[q] & 0xffffffffull), (unsigned)(key[q] >> 32),
+                                                  (unsigned)(cell[q] - strip[q] * kStripCells), __float_as_uint(inten[q]));
+}
+
+constexpr int kBlkMaxRegions = 2048;  // regions of one frame the strip pass can index (2.1 M points)
+
+// One block per (frame, strip): the strip's records — runs in the bin pass's regions, located by
+// a scan of the strip's table column and a binary search over it — reduced in LDS (max key and
+// count per cell), then every cell of the strip written, the top points' intensities gathered
+// first so all those loads are in flight together. (Measured and not adopted: the intensity
+// taken from the records in a second pass over them, no random reads of the points — 144 vs
+// 170 MB per call, but 1,024-thread blocks with 90 KiB of LDS, 56 vs 46 us:
+// profiles/r03f_pmc_bev_blocked_v3_intensity_in_records.json.)
+template <int LAYOUT, bool FLIP>
+__global__ void __launch_bounds__(kStripThreads) bev_blk_strip_kernel(const float4* __restrict__ pts, BevArgs a,
+                                                                      BlkScratch bs, void* __restrict__ out) {
+  constexpr int NT = kStripThreads;
+  __shared__ unsigned long long skey[kStripCells];
+  __shared__ unsigned scnt[kStripCells];
+  __shared__ unsigned pre[kBlkMaxRegions + 1];  // this strip's records before region r
+  __shared__ unsigned short first[kBlkMaxRegions];
+  __shared__ unsigned wsum[NT / 64];
+  const int strip = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  for (int c = tid; c < kStripCells; c += NT) {
+    skey[c] = 0ull;
+    scnt[c] = 0u;
+  }
+  const int nblk = bs.blk0[b + 1] - bs.blk0[b];  // <= kBlkMaxRegions (checked at launch)
+  const size_t reg0 = (size_t)bs.blk0[b];
+  // exclusive scan of the regions' counts of this strip: thread t owns regions [t*per, t*per+per)
+  const int per = (nblk + NT - 1) / NT;
+  unsigned loc = 0;
+  for (int q = 0; q < per; ++q) {
+    const int r = tid * per + q;
+    if (r < nblk) {
+      const unsigned w = bs.tab[(reg0 + r) * kStrips + strip];
+      first[r] = (unsigned short)(w & 0xffffu);
+      loc += w >> 16;
+    }
+  }
+  unsigned x = loc;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned y = __shfl_up(x, d, 64);
+    if ((tid & 63) >= d) x += y;
+  }
+  if ((tid & 63) == 63) wsum[tid >> 6] = x;
+  __syncthreads();  // also: skey / scnt / first written
+  unsigned run = x - loc;
+  for (int w = 0; w < (tid >> 6); ++w) run += wsum[w];
+  for (int q = 0; q < per; ++q) {
+    const int r = tid * per + q;
+    if (r < nblk) {
+      pre[r] = run;
+      run += bs.tab[(reg0 + r) * kStrips + strip] >> 16;
+    }
+  }
+  if (tid == NT - 1) {  // the total: every thread's count
+    unsigned t = 0;
+    for (int w = 0; w < NT / 64; ++w) t += wsum[w];
+    pre[nblk] = t;
+  }
+  __syncthreads();
+  const unsigned total = pre[nblk];
+  // every record of the strip, 4 per thread per round: region by binary search over pre, the 4
+  // loads in flight together, then the LDS max / add
+  for (unsigned base = 0; base < total; base += 4 * NT) {
+    uint4 e[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const unsigned idx = base + u * NT + tid;
+      int lo = 0, hi = nblk - 1;  // last region with pre[r] <= idx
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= idx) lo = mid; else hi = mid - 1;
+      }
+      e[u] = idx < total ? bs.rec[(reg0 + lo) * kBlkPts + first[lo] + (idx - pre[lo])] : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (base + u * NT + tid < total) {
+        atomicMax(&skey[e[u].z], ((unsigned long long)e[u].y << 32) | e[u].x);
+        atomicAdd(&scnt[e[u].z], 1u);
+      }
+  }
+  __syncthreads();
+  // every cell of the strip: the top points' intensities gathered first (all loads in flight),
+  // then the three channels stored
+  constexpr int CPT = (kStripCells + NT - 1) / NT;
+  float inten[CPT];
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+    const int c = tid + q * NT;
+    inten[q] = c < kStripCells ? bev_top_intensity(pts, a, b, scnt[c], skey[c]) : 0.f;
+  }
+#pragma unroll
+  for (int q = 0; q < CPT; ++q) {
+    const int c = tid + q * NT;
+    if (c < kStripCells) bev_store_cell_i<LAYOUT, FLIP>(a, b, strip * kStripCells + c, scnt[c], skey[c], inten[q], out);
+  }
+}
+
 }  // namespace sfa
 
 using namespace sfa;
 
-extern "C" size_t sfa_bev_scratch_size(int batch) {
-  if (batch <= 0) return 0;
+// atomic path: keys + counts per cell; binned path: its counters + records (12 B per cell of
+// room: ~277 k points per frame) after them
+static size_t bev_atomic_bytes(int batch) {
   return align_up((size_t)batch * kBevCells * sizeof(unsigned long long), 256) +
          align_up((size_t)batch * kBevCells * sizeof(unsigned), 256);
+}
+
+extern "C" size_t sfa_bev_scratch_size(int batch) {
+  if (batch <= 0) return 0;
+  return 2 * bev_atomic_bytes(batch);
 }
 
 extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offsets, int batch,
@@ -303,8 +489,9 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
                 SFA_BEV_MAX_BATCH);
   SFA_CHECK_ARG(frame_offsets && boundary && out && scratch, "bev: null argument");
   SFA_CHECK_ARG(out_layout >= 0 && out_layout <= 2, "bev: bad out_layout %d", out_layout);
-  SFA_CHECK_ARG((flags & ~(SFA_BEV_PREFILTERED | SFA_BEV_FLIP_HW | SFA_BEV_FORCE_ATOMIC)) == 0,
+  SFA_CHECK_ARG((flags & ~(SFA_BEV_PREFILTERED | SFA_BEV_FLIP_HW | SFA_BEV_FORCE_ATOMIC | SFA_BEV_FORCE_BINNED)) == 0,
                 "bev: bad flags %d", flags);
+  const int flags_in = flags;
   const bool flip = (flags & SFA_BEV_FLIP_HW) != 0;
   const bool force_atomic = (flags & SFA_BEV_FORCE_ATOMIC) != 0;  // the atomic path (A/B, the equivalence test)
   flags &= SFA_BEV_PREFILTERED;
@@ -341,13 +528,59 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
       reinterpret_cast<char*>(scratch) +
       align_up((size_t)batch * kBevCells * sizeof(unsigned long long), 256));
   const float4* p4 = reinterpret_cast<const float4*>(points);
-  // binned path (default) when the batch's points fit the scratch as 16-B records
+  // blocked-bin path (default) when the batch's regions and table fit the binned scratch
+  {
+    BlkScratch bk;
+    int64_t nblk_total = 0;
+    for (int b = 0; b < batch; ++b) {
+      bk.blk0[b] = (int)nblk_total;
+      nblk_total += (frame_offsets[b + 1] - frame_offsets[b] + kBlkPts - 1) / kBlkPts;
+    }
+    bk.blk0[batch] = (int)nblk_total;
+    const size_t rec_bytes = align_up((size_t)nblk_total * kBlkPts * sizeof(uint4), 256);
+    const size_t tab_bytes = (size_t)nblk_total * kStrips * sizeof(unsigned);
+    // after the binned path's (zero) counters, which it must not touch
+    const size_t cnt_bytes = 3 * align_up((size_t)batch * kStrips * sizeof(unsigned), 256);
+    int max_regions = 0;
+    for (int b = 0; b < batch; ++b) max_regions = std::max(max_regions, bk.blk0[b + 1] - bk.blk0[b]);
+    if (!force_atomic && !(flags_in & SFA_BEV_FORCE_BINNED) && max_regions <= kBlkMaxRegions &&
+        cnt_bytes + rec_bytes + tab_bytes <= bev_atomic_bytes(batch)) {
+      char* sb = reinterpret_cast<char*>(scratch) + bev_atomic_bytes(batch) + cnt_bytes;
+      bk.rec = reinterpret_cast<uint4*>(sb);
+      bk.tab = reinterpret_cast<unsigned*>(sb + rec_bytes);
+      if (max_n > 0) {
+        dim3 g1((unsigned)((max_n + kBlkPts - 1) / kBlkPts), batch);
+        if (flags == SFA_BEV_RAW)
+          hipLaunchKernelGGL(bev_blk_bin_kernel<true>, g1, dim3(kBlkThreads), 0, st, p4, a, bk);
+        else
+          hipLaunchKernelGGL(bev_blk_bin_kernel<false>, g1, dim3(kBlkThreads), 0, st, p4, a, bk);
+        SFA_LAUNCH_CHECK();
+      }
+      dim3 g3(kStrips, batch);
+#define SFA_BEV_BLK(L, F) \
+  hipLaunchKernelGGL((bev_blk_strip_kernel<L, F>), g3, dim3(kStripThreads), 0, st, p4, a, bk, out)
+      switch (out_layout) {
+        case SFA_BEV_NCHW3_F32:
+          if (flip) SFA_BEV_BLK(SFA_BEV_NCHW3_F32, true); else SFA_BEV_BLK(SFA_BEV_NCHW3_F32, false);
+          break;
+        case SFA_BEV_NCHW3_F64:
+          if (flip) SFA_BEV_BLK(SFA_BEV_NCHW3_F64, true); else SFA_BEV_BLK(SFA_BEV_NCHW3_F64, false);
+          break;
+        default:
+          if (flip) SFA_BEV_BLK(SFA_BEV_NHWC4_F32, true); else SFA_BEV_BLK(SFA_BEV_NHWC4_F32, false);
+      }
+#undef SFA_BEV_BLK
+      SFA_LAUNCH_CHECK();
+      return SFA_OK;
+    }
+  }
+  // binned path (round 2) when forced or when the blocked regions do not fit
   const size_t bin_bytes = align_up((size_t)batch * kStrips * sizeof(unsigned), 256);
-  const size_t scratch_bytes = sfa_bev_scratch_size(batch);
+  const size_t binned_bytes = bev_atomic_bytes(batch);  // the binned path's region
   const int64_t total = frame_offsets[batch] - frame_offsets[0];
-  if (!force_atomic && 3 * bin_bytes < scratch_bytes &&
-      (uint64_t)total <= (uint64_t)((scratch_bytes - 3 * bin_bytes) / sizeof(uint4)) && total < (int64_t)0xffffffff) {
-    char* sb = reinterpret_cast<char*>(scratch);
+  if (!force_atomic && 3 * bin_bytes < binned_bytes &&
+      (uint64_t)total <= (uint64_t)((binned_bytes - 3 * bin_bytes) / sizeof(uint4)) && total < (int64_t)0xffffffff) {
+    char* sb = reinterpret_cast<char*>(scratch) + bev_atomic_bytes(batch);
     BinScratch bs;
     bs.count = reinterpret_cast<unsigned*>(sb);
     bs.offset = reinterpret_cast<unsigned*>(sb + bin_bytes);

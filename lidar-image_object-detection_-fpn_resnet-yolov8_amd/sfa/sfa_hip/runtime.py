@@ -383,10 +383,13 @@ class DetectorPipeline:
 
     def __init__(self, engine: KfpnEngine, batch: int, height: int = 608, width: int = 608,
                  K: int = 50, with_bev: bool = False, max_points: int = 0, two_sided: bool = False,
-                 boundary=DEFAULT_BOUNDARY, boundary_back=None):
+                 boundary=DEFAULT_BOUNDARY, boundary_back=None, bev_layout: str = "nchw3"):
         """two_sided (with_bev only): every sweep is also voxelised with ``boundary_back``
         and flipped (demo_2_sides.py: demo_dataset.py:70-88 + demo_utils.py:110-111), so one
-        run infers 2*batch maps: frames [0, batch) front, [batch, 2*batch) back."""
+        run infers 2*batch maps: frames [0, batch) front, [batch, 2*batch) back.
+        bev_layout (with_bev only): the voxeliser's output / the model's input — "nchw3" (the
+        reference's (B, 3, 608, 608) f32, read by the patch stem directly: 3/4 of NHWC4's bytes)
+        or "nhwc4" ((B, 608, 608, 4), channel 3 = 0)."""
         self.engine = engine
         self.dev = engine.device
         self.B, self.H, self.W, self.K = batch, height, width, K
@@ -411,7 +414,13 @@ class DetectorPipeline:
                 if (height, width) != (608, 608):
                     raise ValueError("the BEV grid is 608x608 (config/kitti_config.py:45-46)")
                 self.vox = BevVoxelizer(self.dev, batch)
-                self.bev = torch.empty((nmap, 608, 608, 4), dtype=torch.float32, device=self.dev)
+                if bev_layout not in ("nchw3", "nhwc4"):
+                    raise ValueError(f"bev_layout must be 'nchw3' or 'nhwc4', not {bev_layout!r}")
+                self.bev_layout = bev_layout
+                self.bev_fmt = _lib.BEV_NCHW3_F32 if bev_layout == "nchw3" else _lib.BEV_NHWC4_F32
+                self.in_fmt = _lib.IN_NCHW3 if bev_layout == "nchw3" else _lib.IN_NHWC4
+                shape = (nmap, 3, 608, 608) if bev_layout == "nchw3" else (nmap, 608, 608, 4)
+                self.bev = torch.empty(shape, dtype=torch.float32, device=self.dev)
                 self.points = torch.zeros((max(max_points, 1), 4), dtype=torch.float32,
                                           device=self.dev)
                 self.offsets = np.zeros(batch + 1, np.int64)
@@ -446,11 +455,11 @@ class DetectorPipeline:
         part replays that graph (``_eager`` forces the eager launches: capture() uses it)."""
         st = _lib.stream_ptr(self.dev)
         if self.with_bev:
-            self.vox(self.points, self.offsets, boundary=self.boundary, layout=_lib.BEV_NHWC4_F32,
+            self.vox(self.points, self.offsets, boundary=self.boundary, layout=self.bev_fmt,
                      flags=_lib.BEV_RAW, out=self.bev[: self.B], stream=st)
             if self.two_sided:
                 self.vox(self.points, self.offsets, boundary=self.boundary_back,
-                         layout=_lib.BEV_NHWC4_F32, flags=_lib.BEV_RAW | _lib.BEV_FLIP_HW,
+                         layout=self.bev_fmt, flags=_lib.BEV_RAW | _lib.BEV_FLIP_HW,
                          out=self.bev[self.B:], stream=st)
             if bev_done is not None:
                 bev_done.record(torch.cuda.current_stream(self.dev))
@@ -461,7 +470,7 @@ class DetectorPipeline:
 
     def _infer(self, st):
         if self.with_bev:
-            self.engine.forward_into(self.bev, self.outs, _lib.IN_NHWC4, self.ws, st)
+            self.engine.forward_into(self.bev, self.outs, self.in_fmt, self.ws, st)
         else:
             self.engine.forward_into(self.x, self.outs, _lib.IN_NCHW3, self.ws, st)
         o = self.outs

@@ -11,8 +11,8 @@ k % 2).  Then, for EVERY frame of BOTH pipelines:
 * detections (B, 50, 10) vs the oracle decode of the GPU's own sigmoid maps: bit-exact (same
   maps in, same peaks / top-K / gathers out);
 * ``--workload e2e``: the 16 BEV maps the graph voxelised from raw 132,880-point sweeps vs the
-  oracle makeBEVMap, bit-exact (NHWC4, zero 4th channel), and the logits vs the oracle forward
-  of those maps.
+  oracle makeBEVMap, bit-exact (NCHW3 f32, the layout the patch stem reads), and the logits vs
+  the oracle forward of those maps.
 """
 import numpy as np
 import pytest
@@ -79,11 +79,9 @@ def test_bench_e2e_config_matches_oracle(gpu):
     clouds = [synthetic.synthetic_point_cloud(i + 1) for i in range(16)]
     maps = np.stack([bev_oracle.makeBEVMap(bev_oracle.get_filtered_lidar(c, DEFAULT_BOUNDARY),
                                            DEFAULT_BOUNDARY) for c in clouds])
-    ref_nhwc = maps.astype(np.float32).transpose(0, 2, 3, 1)
     for p in b.pipes:
-        gb = p.bev[:16].cpu().numpy()
-        np.testing.assert_array_equal(gb[..., :3], ref_nhwc)
-        assert not np.any(gb[..., 3])
+        assert p.bev_layout == "nchw3"  # bench's default: the patch stem reads the NCHW3 map
+        np.testing.assert_array_equal(p.bev[:16].cpu().numpy(), maps.astype(np.float32))
     torch.set_num_threads(16)
     with torch.no_grad():
         ref = model_oracle.forward(_oracle_sd(), torch.from_numpy(maps.astype(np.float32)))

@@ -14,6 +14,18 @@ pytestmark = pytest.mark.gpu
 NAMES = ["sweep_s1", "sweep_s2_sub", "kat_edges", "single_point", "empty_after_filter"]
 
 
+def _scratch_clean(vox):
+    """The voxeliser's scratch contract: zero again after every call, except the binned path's
+    record region (written before it is read, never assumed zero). Layout (csrc/bev.hip):
+    atomic keys + counts per cell, then the binned counters [count | offset | cursor], then the
+    records."""
+    B = vox.max_batch
+    al = lambda n: (n + 255) // 256 * 256  # noqa: E731
+    atomic = al(B * 608 * 608 * 8) + al(B * 608 * 608 * 4)
+    bins = 3 * al(B * 76 * 4)
+    return int(vox.scratch[:atomic + bins].count_nonzero()) == 0
+
+
 def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
@@ -56,7 +68,7 @@ def test_scratch_stays_clean_and_repeatable(gpu):
     pts = torch.from_numpy(np.concatenate(clouds)).to(gpu)
     vox = runtime.BevVoxelizer(gpu, 2)
     a = vox(pts, offs, gc.BOUNDARY, layout=_lib.BEV_NCHW3_F64).cpu().numpy()
-    assert int(vox.scratch.count_nonzero()) == 0
+    assert _scratch_clean(vox)
     b = vox(pts, offs, gc.BOUNDARY, layout=_lib.BEV_NCHW3_F64).cpu().numpy()
     np.testing.assert_array_equal(a, b)
     for i, c in enumerate(clouds):
@@ -107,8 +119,9 @@ def test_cpu_input_refused():
 
 @pytest.mark.parametrize("flip", [False, True])
 def test_binned_path_equals_atomic_path(gpu, flip):
-    """The default binned voxeliser (points binned by 8-row strips, each strip reduced in LDS)
-    gives the bits of the global-atomic one (flag SFA_BEV_FORCE_ATOMIC) in every layout, flipped or not,
+    """The default blocked voxeliser (one pass bins each 1024 points by 8-row strips into its own
+    record region + table, each strip reduced in LDS) and round 2's binned one (count / scan /
+    bin / strip, SFA_BEV_FORCE_BINNED) give the bits of the global-atomic one (flag SFA_BEV_FORCE_ATOMIC) in every layout, flipped or not,
     on a ragged batch with a saturated-density cell and an empty frame; both leave the scratch
     zeroed."""
     from sfa_hip import synthetic
@@ -125,10 +138,13 @@ def test_binned_path_equals_atomic_path(gpu, flip):
     vox = runtime.BevVoxelizer(gpu, len(clouds))
     flags = _lib.BEV_RAW | (_lib.BEV_FLIP_HW if flip else 0)
     for layout in (_lib.BEV_NCHW3_F64, _lib.BEV_NCHW3_F32, _lib.BEV_NHWC4_F32):
-        binned = vox(pts, offs, gc.BOUNDARY, layout=layout, flags=flags).cpu().numpy()
-        assert int(vox.scratch.count_nonzero()) == 0
+        blocked = vox(pts, offs, gc.BOUNDARY, layout=layout, flags=flags).cpu().numpy()
+        assert _scratch_clean(vox)
+        binned = vox(pts, offs, gc.BOUNDARY, layout=layout, flags=flags | _lib.BEV_FORCE_BINNED).cpu().numpy()
+        assert _scratch_clean(vox)
         atomic = vox(pts, offs, gc.BOUNDARY, layout=layout, flags=flags | _lib.BEV_FORCE_ATOMIC).cpu().numpy()
-        assert int(vox.scratch.count_nonzero()) == 0
+        assert _scratch_clean(vox)
+        np.testing.assert_array_equal(blocked, atomic)
         np.testing.assert_array_equal(binned, atomic)
     f64 = vox(pts, offs, gc.BOUNDARY, layout=_lib.BEV_NCHW3_F64).cpu().numpy()
     for i, c in enumerate(clouds):
@@ -147,8 +163,8 @@ def test_oversized_frame_uses_atomic_path(gpu):
     pts[:, 2] = rng.uniform(-3, 1.5, n)
     pts[:, 3] = rng.uniform(0, 1, n)
     vox = runtime.BevVoxelizer(gpu, 1)
-    assert n * 16 > vox.scratch.numel()
+    assert n * 16 > vox.scratch.numel() // 2  # the record region: the half after the atomic cells
     got = vox(torch.from_numpy(pts).to(gpu), [0, n], gc.BOUNDARY, layout=_lib.BEV_NCHW3_F64).cpu().numpy()[0]
-    assert int(vox.scratch.count_nonzero()) == 0
+    assert _scratch_clean(vox)
     exp = bev_oracle.makeBEVMap(bev_oracle.get_filtered_lidar(pts, gc.BOUNDARY), gc.BOUNDARY)
     np.testing.assert_array_equal(got, exp)
