@@ -108,7 +108,8 @@ static bool strip_ok(const ConvArgs& a) {
 //    non-strip convs / the strip convs to the round-1 kernels for same-box A/B, bit 32 the FPN
 //    skip convs, bit 64 the heads to the unpacked epilogue, bit 128 the 64-wide strip convs to
 //    no residual prefetch, bit 256 the conv_r3 launches to the tap-major K order, bit 512 the
-//    128..512-wide conv_h3 launches to the 32x32x16 MFMA form;
+//    128..512-wide conv_h3 launches to the 32x32x16 MFMA form; round 3: bit 65536 the heads to
+//    the unstaggered kernel, bit 131072 to the stagger without s_setprio;
 //  * split-K 2 for the 512-wide (layer4) convs, whose 184 tiles cannot fill 256 CUs (-13..16 %);
 //    picked from the width only, so a frame's arithmetic never depends on the batch.
 // conv_x6g_kernel<..., PREC 1> tiles as the fallback.
@@ -133,6 +134,9 @@ constexpr int H3S_128 = 2 | 8;
 constexpr int R3_HEAD = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536 | 524288;  // + v_fma_mix split, 3-block W
                                                                                  // read-ahead, scalar tap decode,
                                                                                  // packed epilogue, chunk-major K
+// + waves 4-7 half a K-tile behind their SIMD partners (three W stages): heads L1 / L2 / L0
+// -4.6 / -3.1 / -1.0 % per launch in isolation, bit-identical (profiles/r03h_convbench_heads_stagger.txt)
+constexpr int R3_HEAD_STAG = R3_HEAD | 1048576;
 
 static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;
@@ -146,8 +150,12 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
         rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD & ~65536>(a, st);
       else if (a.tune & 256)  // tap-major K order (A/B)
         rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD & ~524288>(a, st);
-      else if (!(a.tune & 4))
+      else if (a.tune & 65536)  // round 2: no stagger, two W stages, 3-block read-ahead (A/B)
         rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD>(a, st);
+      else if (a.tune & 131072)  // stagger without the second half's s_setprio (A/B)
+        rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 3, R3_HEAD_STAG & ~4>(a, st);
+      else if (!(a.tune & 4))
+        rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 3, R3_HEAD_STAG>(a, st);
       if (!ok(rc)) rc = launch_conv_h3_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2, 1>(a, st);
       if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 320, 32, EPI_HEAD, 1, 16, 3, 0, 320, 1>(a, st);
     }

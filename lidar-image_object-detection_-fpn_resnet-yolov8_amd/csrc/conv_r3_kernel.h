@@ -391,10 +391,22 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
 // waves of a SIMD (w, w + NW/2) on alternate blocks, so no SIMD issues two DMA bursts at once,
 // 512 = staggered split: waves w < NW/2 split the next tile's A at block SPLIT_AT (into hn),
 // the others at the top of their tile, so after a barrier one wave of each SIMD issues MFMAs
-// while its partner splits.
+// while its partner splits,
+// 1048576 = half-tile stagger (NSTAGE 3, with 256 and 2048): waves NW/2 .. NW - 1 run their K
+// loop half a K-tile behind their SIMD partners (w - NW/2). The barrier that closes interval i
+// (W of tile i + 1 landed) comes after tile i for the first half of the waves and after the
+// first half of tile i for the second, so the partners never reach their split VALU, their
+// tile-top W reads and the barrier wait together: while one waits or splits, the other issues
+// MFMAs. Interval i reads tiles i - 1 (second half only) and i, and DMAs tile i + 1: three
+// stages. The delayed half reads the next tile's first W blocks ahead across its tile boundary
+// (that tile was published by the barrier before); the leading half reads them after its
+// barrier. Same products in the same order: bit-identical to the unstaggered loop.
 template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int NSEG, int ABL = 0>
 __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const ConvArgs a) {
   static_assert(NSTAGE == 2 || NSTAGE == 3, "W ring depth");
+  constexpr bool STAG = (ABL & 1048576) != 0;
+  static_assert(!STAG || (NSTAGE == 3 && (ABL & 256) != 0 && (ABL & 2048) != 0 && (ABL & (8 | 16 | 32 | 64 | 128 | 512)) == 0),
+                "stagger: NSTAGE 3, spread W DMA, transposed accumulators, no split / schedule ablations");
   static_assert(NSEG == 1 || NSEG == 2, "segments");
   static_assert(EPI == EPI_STD || EPI == EPI_HEAD, "epilogue");
   constexpr int NW = BM / WM, NT = NW * 64;
@@ -603,7 +615,8 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   const int bfo = c16 * BROW + ((g ^ swzB(c16)) << 4);  // this lane's W fragment in a block
   constexpr int RA = (ABL & 8192) != 0 ? 3 : 2;  // W fragment blocks read ahead of their MFMAs
   constexpr int RS = RA + 1;
-  static_assert(RA == 2 || NSTAGE == 2, "3-block read-ahead: NSTAGE 2 only");
+  static_assert(RA == 2 || NSTAGE == 2 || STAG, "3-block read-ahead: NSTAGE 2 only");
+  static_assert(!STAG || (TN % RS == 0 && TN % 2 == 0 && TN / 2 > RA), "stagger: W ring slots must repeat per tile");
   f16x8_t bq[RS][2];  // W fragment ring: block p in slot p % RS
   auto read_b = [&](const unsigned char* S, int ni, f16x8_t (&dst)[2]) {
     dst[0] = *reinterpret_cast<const f16x8_t*>(S + bfo + ni * 16 * BROW);
@@ -615,7 +628,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   constexpr int NA_OPS = 2 * TM;  // A loads per K-tile (issued after the tile's W DMA)
   // prologue: W tiles 0 .. NSTAGE-2, A tile 0; this wave's W landed, then everyone's
 #pragma unroll
-  for (int p = 0; p < NSTAGE - 1; ++p)
+  for (int p = 0; p < (STAG ? NSTAGE - 2 : NSTAGE - 1); ++p)
     if (p < nk) load_w(kt0 + p, smem + p * STAGE);
   load_a(kt0);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA_OPS) : "memory");
@@ -624,7 +637,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   if constexpr ((ABL & 512) != 0) {
     if (wave >= NW / 2 ? 0 : 1) split_a(hf);
   }
-  if constexpr (NSTAGE == 3) {
+  if constexpr (NSTAGE == 3 && !STAG) {
     read_b(smem, 0, bq[0]);
     read_b(smem, 1, bq[1]);
   }
@@ -632,8 +645,83 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
     if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   }
   const int wave_half = wave >= NW / 2 ? 1 : 0;  // SIMD partners: waves w and w + NW / 2
+  auto mma_block = [&](int ni) {
+    const f16x8_t c0 = bq[ni % RS][0], c1 = bq[ni % RS][1];
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      f32x4_t cc = acc[mi][ni];
+      cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[1][mi], cc, 0, 0, 0);
+      cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c1, hf[0][mi], cc, 0, 0, 0);
+      cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[0][mi], cc, 0, 0, 0);
+      acc[mi][ni] = cc;
+    }
+  };
+  // stagger (see the ABL list): the K loop of one half of the waves, HB = the delayed half.
+  // Interval i = the steps between barriers i - 1 and i; a block's interval-relative position r
+  // places the W DMA pieces (slot s at r = 2 + 2 s + HB, as ABL 256 spreads them) of tile i + 1.
+  auto stag_loop = [&](auto hb_c) {
+    constexpr bool HB = decltype(hb_c)::value;
+    constexpr int H2 = TN / 2;
+    constexpr int SLOTS = (TN - 2) / 2 >= 1 ? (TN - 2) / 2 : 1;
+    constexpr int PPB = (NB + SLOTS - 1) / SLOTS;
+    auto dma_slot = [&](int s, int tile, unsigned char* S) {
+#pragma unroll
+      for (int jj = 0; jj < PPB; ++jj) {
+        const int j = s * PPB + jj;
+        if (j < NB) load_w_piece(j, tile, S);
+      }
+    };
+    int st_cur = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const unsigned char* S = smem + st_cur * STAGE;
+      const int st_n1 = st_cur + 1 == NSTAGE ? 0 : st_cur + 1;
+      const int st_n2 = st_n1 + 1 == NSTAGE ? 0 : st_n1 + 1;
+      const bool more_a = kt + 1 < nk;
+      split_a(hf);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!HB || kt == 0) {
+#pragma unroll
+        for (int p = 0; p < RA; ++p) read_b(S, p, bq[p % RS]);
+      }
+      if (HB && kt == 0 && more_a) {
+        // the delayed half's pieces of tile 1 whose slots fall before its first tile (r < H2)
+#pragma unroll
+        for (int s = 0; s < SLOTS; ++s)
+          if (3 + 2 * s < H2) dma_slot(s, kt0 + 1, smem + st_n1 * STAGE);
+      }
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        if (ni == 0 && more_a && !(ABL & 131072)) load_a(kt0 + kt + 1);
+        {
+          const bool late = HB && ni >= H2;                   // block in interval kt + 1
+          const int r = HB ? (late ? ni - H2 : ni + H2) : ni;  // compile-time for each HB
+          const int tw = late ? kt + 2 : kt + 1;               // tile DMA'd in this interval
+          if (r >= 2 && ((r - 2) & 1) == (HB ? 1 : 0) && ((r - 2) >> 1) < SLOTS && tw < nk && !(ABL & 1))
+            dma_slot((r - 2) >> 1, kt0 + tw, smem + (late ? st_n2 : st_n1) * STAGE);
+        }
+        const int p = ni + RA;
+        if (p < TN)
+          read_b(S, p, bq[p % RS]);
+        else if (HB && more_a)
+          read_b(smem + st_n1 * STAGE, p - TN, bq[p % RS]);
+        mma_block(ni);
+        if (ni == (HB ? H2 - 1 : TN - 1)) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      st_cur = st_n1;
+    }
+  };
+  if constexpr (STAG) {
+    if (wave_half)
+      stag_loop(std::true_type{});
+    else
+      stag_loop(std::false_type{});
+  }
   int st_cur = 0;
-  for (int kt = 0; kt < nk; ++kt) {
+  for (int kt = 0; kt < (STAG ? 0 : nk); ++kt) {
     const unsigned char* S = smem + st_cur * STAGE;
     const int st_nx = st_cur + 1 == NSTAGE ? 0 : st_cur + 1;
     const int st_w = st_cur == 0 ? NSTAGE - 1 : st_cur - 1;  // stage of tile kt + NSTAGE - 1

@@ -288,7 +288,26 @@ def test_round2_kernels_match_round1(golden, gpu, hw):
         assert e <= 1e-4, h
 
 
-@pytest.mark.parametrize("tune", [0, 28, 32, 256, 512])
+@pytest.mark.parametrize("hw", [(160, 192), (96, 96), (608, 608)])
+def test_heads_stagger_bit_identical(golden, gpu, hw):
+    """The heads conv with waves 4-7 half a K-tile behind their SIMD partners (three W stages, the
+    default; OPT_CONV_TUNE bit 131072 without the second half's s_setprio) adds the same products
+    in the same order as the unstaggered kernel (bit 65536): bit-identical outputs. Odd sizes
+    cover partial tiles; K-tile counts 18 / 36 / 72 (C = 64 / 128 / 256) both parities."""
+    x = torch.from_numpy(synthetic.synthetic_bev(2, hw[0], hw[1], seed=37)).to(gpu)
+    outs = []
+    for flag in (0, 65536, 131072):
+        model = make_model(golden, gpu)
+        model._engine(gpu).set_option(_lib.OPT_CONV_TUNE, flag)
+        model._engine(gpu).set_math(_math("fp16x3"))
+        with torch.no_grad():
+            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(outs[1][h], outs[0][h], err_msg=h)
+        np.testing.assert_array_equal(outs[2][h], outs[0][h], err_msg=h)
+
+
+@pytest.mark.parametrize("tune", [0, 28, 32, 256, 512, 65536])
 def test_batch_invariance_608(golden, gpu, tune):
     """At the full 608x608 size (every kernel path of the bench: r3 heads, strip convs, FPN skip
     convs, r3 body convs (M >= 50000 needs >= 9 frames), split-K layer4): frames 7, 8 of a batch

@@ -271,7 +271,8 @@ int main(int argc, char** argv) {
   std::vector<Cand> heads = {
       CANDR(256, 320, 32, EPI_HEAD, 1, 2, 620804, 1), CANDR(128, 320, 32, EPI_HEAD, 2, 2, 620804, 1),
       CANDR(192, 320, 32, EPI_HEAD, 1, 2, 620804, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 620804, 1),
-      CANDR(128, 320, 32, EPI_HEAD, 2, 2, 620804, 1),
+      CANDR(128, 320, 32, EPI_HEAD, 2, 2, 620804, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669376, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
