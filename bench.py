@@ -354,8 +354,8 @@ def probe_heads(args, pipe, step):
 
 
 def probe_bev(args, pipe, reps=20):
-    """configs[2]: the BEV voxelisation pass alone (filter fused; sfa_bev_voxelize's binned
-    count / scan / bin / strip kernels) on the pipeline's resident sweeps, HIP events on the launching stream,
+    """configs[2]: the BEV voxelisation pass alone (filter fused; sfa_bev_voxelize's blocked
+    bin + strip kernels) on the pipeline's resident sweeps, HIP events on the launching stream,
     against the HBM roofline: algorithmic bytes = N * 16 (xyzi read) + 3 * 608^2 * 4 (f32 map
     written) per frame; scratch key / count traffic is not algorithmic."""
     if args.workload != "e2e":
@@ -387,9 +387,11 @@ def probe_bev(args, pipe, reps=20):
     return {"bound": "hbm", "unit": "GB/s", "achieved": round(ach, 1), "peak": 8000.0,
             "frac": round(ach / 8000.0, 4), "traffic": traffic,
             "traffic_basis": "PMC 2 x FETCH_SIZE + WRITE_SIZE of one call (profiles/r*_pmc_bev.json): points read "
-                             "twice (count + bin), 16-B records written and read, the NHWC4 map's 4th channel",
-            "kernel": "sfa_bev_voxelize (SFA_BEV_RAW: filter fused; bev_bin_count / bev_bin_scan / bev_bin / "
-                      "bev_strip kernels, 8-row strips reduced in LDS)",
+                             "once by the bin pass, 16-B records written and read once, the top points' intensities "
+                             "gathered, the NCHW3 f32 map written",
+            "kernel": "sfa_bev_voxelize (SFA_BEV_RAW: filter fused; bev_blk_bin_kernel: 1024 points per block "
+                      "binned by 8-row strip into the block's record region; bev_blk_strip_kernel: each strip "
+                      "reduced in LDS)",
             "us_per_batch": round(1e3 * ms, 1), "points_per_batch": npts,
             "algorithmic_bytes_per_batch": algo,
             "measured": "HIP events around %d back-to-back voxelisations of the step's %d sweeps, "

@@ -162,6 +162,13 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_HEAD, 1, 16, 3, 0, 64, 1>(a, st);
     return rc;
   }
+  if (a.res_up && !(a.tune & 32) && (a.tune & 1048576)) {  // A/B: the residual's taps before the K loop
+    if (a.N == 64)
+      rc = launch_conv_r3_cfg<128, 64, 32, EPI_STD, 3, 2, R3_FPN | 4194304>(a, st);
+    else if (a.N % 128 == 0)
+      rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_FPN | 4194304>(a, st);
+    if (ok(rc)) return rc;
+  }
   if (a.res_up && !(a.tune & 32)) {  // FPN skip convs: transposed float4 epilogue, float4 taps
     if (a.N == 64)
       rc = launch_conv_r3_cfg<128, 64, 32, EPI_STD, 4, 2, R3_FPN>(a, st);

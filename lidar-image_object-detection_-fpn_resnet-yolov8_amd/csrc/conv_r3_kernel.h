@@ -62,6 +62,40 @@ constexpr int r3t_stage_bytes() {
   return (NT / 64) * (TM * 16) * (TN * 64 + 16) + 2 * (NT / 64) * 4;
 }
 
+// The upsampled half-resolution residual (a.res_up) of the lane's rows and channels, bilinear x2
+// with align_corners as res_up_sample evaluates it (4 float4 taps per lane and column block).
+template <int TM, int TN>
+__device__ __forceinline__ void r3t_res_up_load(const ConvArgs& a, x6_f32x4 (&rv)[TM][TN], int mrow0, int n0, int lane) {
+#pragma clang fp contract(off)
+  const int M = a.M, c16 = lane & 15, g = lane >> 4;
+  const int H = a.OH >> 1, W = a.OW >> 1;
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+    const int m = min(mrow0 + mi * 16 + c16, M - 1);
+    const int ow = m % a.OW, t = m / a.OW;
+    const int oh = t % a.OH, b = t / a.OH;
+    const float fy = a.res_sh * (float)oh, fx = a.res_sw * (float)ow;
+    const int y0 = (int)fy, x0 = (int)fx;
+    const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+    const float ly1 = fy - (float)y0, lx1 = fx - (float)x0;
+    const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+    const float* r = a.res_up + (size_t)b * H * W * a.N;
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      const int n = n0 + ni * 16 + 4 * g;
+      const x6_f32x4 a00 = *reinterpret_cast<const x6_f32x4*>(r + (size_t)(y0 * W + x0) * a.N + n);
+      const x6_f32x4 a01 = *reinterpret_cast<const x6_f32x4*>(r + (size_t)(y0 * W + x1) * a.N + n);
+      const x6_f32x4 a10 = *reinterpret_cast<const x6_f32x4*>(r + (size_t)(y1 * W + x0) * a.N + n);
+      const x6_f32x4 a11 = *reinterpret_cast<const x6_f32x4*>(r + (size_t)(y1 * W + x1) * a.N + n);
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        rv[mi][ni][v] = fmaf(ly0, fmaf(lx0, a00[v], lx1 * a01[v]), ly1 * fmaf(lx0, a10[v], lx1 * a11[v]));
+    }
+  }
+}
+
+// PRE: the residual tile (a.res, or with RU the upsampled a.res_up) was loaded by the caller
+// (r3t_res_load / r3t_res_up_load) into `pre`, so its latency hid behind the MFMAs.
 template <int TM, int TN, int NT, bool RU = false, bool PRE = false, int EABL = 0, bool STG = false>
 __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
                                                  int mrow0, int m0, int n0, int lane, const float (&ainv)[TM],
@@ -76,7 +110,12 @@ __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&ac
   unsigned char* const stg = smem + (threadIdx.x >> 6) * (TM * 16) * PITCH;
   AmaxRows am(a.OH * a.OW, m0);
   x6_f32x4 rv[TM][TN];
-  if (RU && a.res_up) {
+  if (PRE && RU && a.res_up) {
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) rv[mi][ni] = pre[mi][ni];
+  } else if (RU && a.res_up) {
     const int H = a.OH >> 1, W = a.OW >> 1;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
@@ -631,6 +670,13 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   for (int p = 0; p < (STAG ? NSTAGE - 2 : NSTAGE - 1); ++p)
     if (p < nk) load_w(kt0 + p, smem + p * STAGE);
   load_a(kt0);
+  // RUP (4194304, with 32768): the upsampled residual's taps loaded and interpolated before the
+  // K loop (one latency with the first tiles' loads instead of one more after the MFMAs)
+  constexpr bool RUP = (ABL & 4194304) != 0 && (ABL & 32768) != 0 && (ABL & 2048) != 0 && EPI == EPI_STD;
+  x6_f32x4 rup[RUP ? TM : 1][RUP ? TN : 1];
+  if constexpr (RUP) {
+    if (a.res_up) r3t_res_up_load<TM, TN>(a, rup, m0 + wave * WM, n0, lane);
+  }
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA_OPS) : "memory");
   __builtin_amdgcn_s_barrier();
   if constexpr ((ABL & 48) != 0) split_a(hf);
@@ -877,6 +923,10 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   if constexpr ((ABL & 2048) != 0) {
     if constexpr (EPI == EPI_HEAD)
       r3t_epilogue_head<TM, TN, NT, BN / 64, (ABL & 65536) != 0>(a, acc, smem, m0 + wave * WM, n0, nt, tid, ainv);
+    else
+    if constexpr (RUP)
+      r3t_epilogue_std<TM, TN, NT, true, true, (ABL & 262144) ? 4 : 0>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv,
+                                                                        rup);
     else
       r3t_epilogue_std<TM, TN, NT, (ABL & 32768) != 0, false, (ABL & 262144) ? 4 : 0>(a, acc, smem, m0 + wave * WM, m0, n0,
                                                                                       lane, ainv);

@@ -394,6 +394,264 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs 
   }
 }
 
+// Round 3b: the same conv, scales and pool, one barrier per tile (stem_patch_pool_kernel has
+// three), the pool computed from the accumulators instead of a 64 KiB LDS image of the tile.
+//  * Patches double-buffered in LDS: tile t's MFMAs read patch buffer t & 1 while the split of
+//    tile t + G's patch (its max reduced before the previous barrier) goes to the other one.
+//  * Pool: lane (c, g) of a wave holds conv columns 4g .. 4g + 3 of rows 2w, 2w + 1 for channels
+//    16 ni + c. Horizontal 3-maxima of the pooled columns 2g, 2g + 1 (and 8 for g = 3) come from
+//    the lane's own values and column 4g - 1 of lane l - 16 (one bpermute per value); the vertical
+//    3-maximum of pooled row w needs conv row 2w - 1, wave w - 1's second row: every wave
+//    publishes its second row's horizontal maxima (9 x 64 floats) in an exchange buffer, and
+//    after the tile's barrier each wave finishes its pooled row from registers + that buffer
+//    (wave 7 also the row-8 partials). Ownership, side-buffer slots and the merge pass are
+//    stem_pool_epilogue's (side-buffer mode only); the values are the same maxima of the same
+//    ReLU(fmaf(acc, winv / s, b)) values: bit-identical output.
+//  * Per tile, between barriers: the previous tile's pooled row (stores), the next patch's split,
+//    this tile's MFMAs, its ReLU / horizontal maxima / exchange writes, the max of the patch two
+//    ahead. ABL 1: waves 4-7 issue their MFMAs first and the previous tile's stores and the split
+//    after them, so the two waves of a SIMD do not reach their MFMAs together.
+namespace stem_patch2 {
+using namespace stem_patch;
+constexpr int XCH_W = 9 * 64 * 4;                  // one wave's second-row horizontal maxima
+constexpr int XCH_BYTES = NW * XCH_W;              // per buffer
+constexpr int LDS2 = W_BYTES + 2 * 2 * PATCH_TERM + 2 * XCH_BYTES + 2 * 2 * NW * 4;  // 141,376 B
+}  // namespace stem_patch2
+
+template <int IN = STEM_IN_NHWC4, int ABL = 0>
+__global__ void __launch_bounds__(512, 1) stem_patch_pool2_kernel(const ConvArgs a, int ntiles) {
+#pragma clang fp contract(off)
+  using namespace stem_patch2;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS2];
+  unsigned char* SW = smem;
+  unsigned char* SU0 = smem + W_BYTES;                              // patch buffers: [2][2 terms]
+  float* XCH0 = reinterpret_cast<float*>(SU0 + 4 * PATCH_TERM);      // [2][NW][9][64]
+  float* WMX = XCH0 + 2 * XCH_BYTES / 4;                             // [2][NW] patch maxima
+  float* TMX = WMX + 2 * NW;                                         // [2][NW] tile (ReLU) maxima
+  const ConvSeg& g = a.seg[0];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tw_n = a.OW / TW, tiles_per_frame = (a.OH / TH) * tw_n;
+  const int PHo = a.OH >> 1, PWo = a.OW >> 1;
+
+  x6_f32x4 R0[PF], R1[PF];
+  auto fetch = [&](int tile, x6_f32x4 (&pf)[PF]) {
+    const int b = tile / tiles_per_frame, tl = tile - b * tiles_per_frame;
+    const int th = tl / tw_n, tw = tl - th * tw_n;
+    const int iy0 = 2 * TH * th - 3, ix0 = 2 * TW * tw - 3;
+    const size_t hw = (size_t)g.H * g.W;
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int p = tid + j * NT;
+      const int py = p / PW, px = p - py * PW;
+      const int iy = iy0 + py, ix = ix0 + px;
+      x6_f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (p < PIX && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W) {
+        if constexpr (IN == STEM_IN_NHWC4) {
+          v = reinterpret_cast<const x6_f32x4*>(g.x)[(size_t)b * hw + iy * g.W + ix];
+        } else {
+          const int sy = IN == STEM_IN_NCHW3_FLIP ? g.H - 1 - iy : iy;
+          const int sx = IN == STEM_IN_NCHW3_FLIP ? g.W - 1 - ix : ix;
+          const float* x = g.x + (size_t)b * 3 * hw + (size_t)sy * g.W + sx;
+          v[0] = x[0];
+          v[1] = x[hw];
+          v[2] = x[2 * hw];
+        }
+      }
+      pf[j] = v;
+    }
+  };
+  auto patch_max = [&](const x6_f32x4 (&pf)[PF], float* dst) {
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < PF; ++j)
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(pf[j][0]), fabsf(pf[j][1])), fmaxf(fabsf(pf[j][2]), fabsf(pf[j][3]))));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (lane == 0) dst[wave] = m;
+  };
+  // scale of a patch from its published per-wave maxima; split into patch buffer SU
+  auto split_patch = [&](const float* wm, const x6_f32x4 (&pf)[PF], unsigned char* SU) -> float {
+    float tmax = wm[0];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) tmax = fmaxf(tmax, wm[w]);
+    float ainv;
+    const float s = amax_scale_bits(__float_as_uint(tmax), ainv);
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int p = tid + j * NT;
+      if (p < PIX) {
+        f16x4_t hi, lo;
+        split2h(pf[j], s, hi, lo);
+        *reinterpret_cast<f16x4_t*>(SU + p * 8) = hi;
+        *reinterpret_cast<f16x4_t*>(SU + PATCH_TERM + p * 8) = lo;
+      }
+    }
+    return ainv;
+  };
+
+  const int G = gridDim.x;
+  const int t0 = blockIdx.x;
+  if (t0 < ntiles) fetch(t0, R0);
+  if (t0 + G < ntiles) fetch(t0 + G, R1);
+  // weights: wh [2][64][Kpad], k = (kh 7 + kw) 4 + c  ->  LDS [2][64][WROW] at k' = (kh 8 + kw) 4 + c
+  for (int i = tid; i < 2 * 64 * 56; i += NT) {
+    const int t = i / (64 * 56), rem = i - t * (64 * 56);
+    const int n = rem / 56, tap = rem - n * 56;
+    const int kh = tap >> 3, kw = tap & 7;
+    uint2 v = make_uint2(0u, 0u);
+    if (kw < 7) v = *reinterpret_cast<const uint2*>(a.wh + ((size_t)t * 64 + n) * a.Kpad + (kh * 7 + kw) * 4);
+    *reinterpret_cast<uint2*>(SW + t * 64 * WROW + n * WROW + tap * 8) = v;
+  }
+  if (t0 >= ntiles) return;  // uniform per block
+  patch_max(R0, WMX);
+  __syncthreads();
+  float ainv_cur = split_patch(WMX, R0, SU0);
+  if (t0 + 2 * G < ntiles) fetch(t0 + 2 * G, R0);
+  if (t0 + G < ntiles) patch_max(R1, WMX + NW);
+  __syncthreads();
+
+  const int c16 = lane & 15, g4 = lane >> 4;
+  const int abase16 = ((2 * (2 * wave)) * PW + 2 * c16 + 2 * g4) * 8;
+  const int bbase16 = c16 * WROW + 16 * g4;
+  // the previous tile's horizontal maxima: [mi][ni][k], k = pooled column 2 g4, 2 g4 + 1, 8 (g4 = 3)
+  float hp[2][4][3];
+  int prev_tile = -1;
+
+  auto finish_prev = [&](int par) {  // vertical maxima + stores of tile prev_tile (exchange buffer par)
+    if (prev_tile < 0) return;
+    const int b = prev_tile / tiles_per_frame, tl = prev_tile - b * tiles_per_frame;
+    const int th = tl / tw_n, tw = tl - th * tw_n;
+    const float* X = XCH0 + par * (XCH_BYTES / 4);
+    const int tlg = (b * (a.OH >> 4) + th) * (a.OW >> 4) + tw;  // side-buffer tile index
+    const int py = 8 * th + wave;                                // pooled row j = wave
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = ni * 16 + c16;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        if (k == 2 && g4 != 3) continue;
+        const int i = k == 2 ? 8 : 2 * g4 + k;
+        float v = fmaxf(hp[0][ni][k], hp[1][ni][k]);
+        if (wave > 0) v = fmaxf(v, X[((wave - 1) * 9 + i) * 64 + n]);
+        const int px = 8 * tw + i;
+        if (py < PHo && px < PWo) {
+          if (i <= 7)
+            a.y[((size_t)(b * PHo + py) * PWo + px) * 64 + n] = v;
+          else
+            a.part[((size_t)tlg * 17 + 9 + wave) * 64 + n] = v;
+        }
+        if (wave == NW - 1) {  // pooled row 8: conv row 15 only -> the lower neighbour's slot i
+          const int py8 = 8 * th + 8;
+          if (py8 < PHo && px < PWo) a.part[((size_t)tlg * 17 + i) * 64 + n] = hp[1][ni][k];
+        }
+      }
+    }
+    if (tid == 0 && a.amax_out) {
+      const float* tm = TMX + par * NW;
+      float m = tm[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) m = fmaxf(m, tm[w]);
+      if (m > 0.f) amax_atomic(a.amax_out, b, m);
+    }
+  };
+
+  int k = 0;
+  for (int tile = t0; tile < ntiles; tile += G, ++k) {
+    const int par = k & 1;
+    unsigned char* SUc = SU0 + par * 2 * PATCH_TERM;
+    unsigned char* SUn = SU0 + (par ^ 1) * 2 * PATCH_TERM;
+    const bool has_next = tile + G < ntiles;
+    float ainv_next = 0.f;
+    auto prep_next = [&]() {  // the next tile's patch into the other buffer; refill its registers
+      if (!has_next) return;
+      if (par == 0) {
+        ainv_next = split_patch(WMX + NW, R1, SUn);
+        if (tile + 3 * G < ntiles) fetch(tile + 3 * G, R1);
+      } else {
+        ainv_next = split_patch(WMX, R0, SUn);
+        if (tile + 3 * G < ntiles) fetch(tile + 3 * G, R0);
+      }
+    };
+    const bool late = (ABL & 1) != 0 && wave >= NW / 2;
+    if (!late) {
+      finish_prev(par ^ 1);
+      prep_next();
+    }
+    // MFMAs (stem_patch_pool_kernel's 16x16x32 form)
+    f32x4_t acc[2][4];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KP / 32; ++s) {
+      f16x8_t ahi[2], alo[2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const int aoff = abase16 + (2 * mi * PW + s * PW) * 8;
+        ahi[mi] = *reinterpret_cast<const f16x8_t*>(SUc + aoff);
+        alo[mi] = *reinterpret_cast<const f16x8_t*>(SUc + PATCH_TERM + aoff);
+      }
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const unsigned char* wb = SW + bbase16 + ni * 16 * WROW + 64 * s;
+        const f16x8_t whi = *reinterpret_cast<const f16x8_t*>(wb);
+        const f16x8_t wlo = *reinterpret_cast<const f16x8_t*>(wb + 64 * WROW);
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi) {
+          f32x4_t cc = acc[mi][ni];
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(alo[mi], whi, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[mi], wlo, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ahi[mi], whi, cc, 0, 0, 0);
+          acc[mi][ni] = cc;
+        }
+      }
+    }
+    if (late) {
+      finish_prev(par ^ 1);
+      prep_next();
+    }
+    // ReLU(conv * winv / s + b); horizontal maxima; the second row's into the exchange buffer
+    float mx = 0.f;
+    float* X = XCH0 + par * (XCH_BYTES / 4) + wave * 9 * 64;
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = ni * 16 + c16;
+      const float bn = a.bias[n];
+      const float cs = a.winv[n] * ainv_cur;
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float t = fmaf(acc[mi][ni][e], cs, bn);
+          v[e] = t > 0.f ? t : 0.f;
+          mx = fmaxf(mx, v[e]);
+        }
+        const float left = __shfl_up(v[3], 16, 64);  // column 4 g4 - 1 (lane l - 16); unused for g4 = 0
+        hp[mi][ni][0] = g4 > 0 ? fmaxf(fmaxf(left, v[0]), v[1]) : fmaxf(v[0], v[1]);
+        hp[mi][ni][1] = fmaxf(fmaxf(v[1], v[2]), v[3]);
+        hp[mi][ni][2] = v[3];
+        if (mi == 1) {
+          X[(2 * g4) * 64 + n] = hp[1][ni][0];
+          X[(2 * g4 + 1) * 64 + n] = hp[1][ni][1];
+          if (g4 == 3) X[8 * 64 + n] = v[3];
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0) TMX[par * NW + wave] = mx;
+    // the max of the patch two tiles ahead (its registers were refilled during the previous tile)
+    if (tile + 2 * G < ntiles) patch_max(par == 0 ? R0 : R1, WMX + par * NW);
+    prev_tile = tile;
+    ainv_cur = ainv_next;
+    __syncthreads();
+  }
+  finish_prev((k - 1) & 1);
+}
+
 // Grid = one block per CU (each loops over tiles); needs the stem's fp16x3 split weights
 // (Kpad >= 196), the input as a.stem_in says (seg 0 describes it as 4 channels), conv output
 // divisible into 16 x 16 tiles.
@@ -432,6 +690,22 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
     case 16: hipLaunchKernelGGL((stem_patch_pool_kernel<16, NC3>), gd, bd, 0, st, a, ntiles); break;
     case 64: hipLaunchKernelGGL((stem_patch_pool_kernel<64, NC3>), gd, bd, 0, st, a, ntiles); break;
     default:
+      if (a.part && (a.tune & 524288) && a.stem_in == STEM_IN_NCHW3) {  // A/B: waves 4-7 MFMAs first
+        hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3, 1>), gd, bd, 0, st, a, ntiles);
+        break;
+      }
+      if (a.part && !(a.tune & 262144)) {  // round 3b: one barrier per tile (A/B: tune bit 262144)
+        switch (a.stem_in) {
+          case STEM_IN_NCHW3:
+            hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3>), gd, bd, 0, st, a, ntiles);
+            break;
+          case STEM_IN_NCHW3_FLIP:
+            hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3_FLIP>), gd, bd, 0, st, a, ntiles);
+            break;
+          default: hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NHWC4>), gd, bd, 0, st, a, ntiles); break;
+        }
+        break;
+      }
       switch (a.stem_in) {
         case STEM_IN_NCHW3: hipLaunchKernelGGL((stem_patch_pool_kernel<0, STEM_IN_NCHW3>), gd, bd, 0, st, a, ntiles); break;
         case STEM_IN_NCHW3_FLIP:

@@ -402,6 +402,54 @@ def test_stem_input_layouts_bit_exact(golden, gpu, hw):
         assert float(np.max(np.abs(a[h] - r) / np.maximum(1.0, np.abs(r)))) <= 1e-4, h
 
 
+@pytest.mark.parametrize("hw", [(96, 96), (160, 192), (608, 608)])
+def test_stem_one_barrier_bit_identical(golden, gpu, hw):
+    """The one-barrier stem (double-buffered patches, pool from the accumulators + a row exchange:
+    the default) == round 3's three-barrier stem (OPT_CONV_TUNE bit 262144) == its variant with
+    waves 4-7 issuing their MFMAs first (bit 524288), bit for bit, for every head; NHWC4 and
+    flipped-NCHW3 reads through the default kernel too. Sizes with 3 x 3, 5 x 6 and 19 x 19
+    tiles per frame (frame, tile-row and tile-column borders of the pooled side buffer); 3
+    frames so a block's tiles span frames."""
+    x = torch.from_numpy(synthetic.synthetic_bev(3, hw[0], hw[1], seed=53)).to(gpu)
+    outs = []
+    for flag in (0, 262144, 524288):
+        model = make_model(golden, gpu)
+        eng = model._engine(gpu)
+        eng.set_option(_lib.OPT_CONV_TUNE, flag)
+        eng.set_math(_math("fp16x3"))
+        with torch.no_grad():
+            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
+            if flag == 0:
+                nhwc4 = torch.zeros((3, hw[0], hw[1], 4), dtype=torch.float32, device=gpu)
+                nhwc4[..., :3] = x.permute(0, 2, 3, 1)
+                o = eng.alloc_outputs(3, hw[0], hw[1])
+                eng.forward_into(nhwc4, o, _lib.IN_NHWC4)
+                nh = {h: v.cpu().numpy() for h, v in o.items()}
+                fl = {h: v.cpu().numpy() for h, v in
+                      model.forward_layout(torch.flip(x, [2, 3]).contiguous(), _lib.IN_NCHW3_FLIP_HW).items()}
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(outs[0][h], outs[1][h], err_msg=f"{h}: one-barrier vs three-barrier stem")
+        np.testing.assert_array_equal(outs[2][h], outs[1][h], err_msg=f"{h}: MFMAs-first variant")
+        np.testing.assert_array_equal(nh[h], outs[0][h], err_msg=f"{h}: NHWC4")
+        np.testing.assert_array_equal(fl[h], outs[0][h], err_msg=f"{h}: flipped NCHW3")
+
+
+@pytest.mark.parametrize("hw", [(160, 192), (608, 608)])
+def test_fpn_residual_prefetch_bit_identical(golden, gpu, hw):
+    """FPN skip convs with the upsampled residual's taps loaded and interpolated before the K
+    loop (OPT_CONV_TUNE bit 1048576) == the default (taps in the epilogue), bit for bit."""
+    x = torch.from_numpy(synthetic.synthetic_bev(2, hw[0], hw[1], seed=59)).to(gpu)
+    outs = []
+    for flag in (0, 1048576):
+        model = make_model(golden, gpu)
+        model._engine(gpu).set_option(_lib.OPT_CONV_TUNE, flag)
+        model._engine(gpu).set_math(_math("fp16x3"))
+        with torch.no_grad():
+            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(outs[1][h], outs[0][h], err_msg=h)
+
+
 def test_split_k_in_kernel_combine(golden, gpu):
     """Experimental in-kernel split-K (OPT_CONV_TUNE bit 1024: the last slice to arrive adds the
     others' partials in slice order) is bit-identical to the same split through the separate
