@@ -690,11 +690,11 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
     case 16: hipLaunchKernelGGL((stem_patch_pool_kernel<16, NC3>), gd, bd, 0, st, a, ntiles); break;
     case 64: hipLaunchKernelGGL((stem_patch_pool_kernel<64, NC3>), gd, bd, 0, st, a, ntiles); break;
     default:
-      if (a.part && (a.tune & 524288) && a.stem_in == STEM_IN_NCHW3) {  // A/B: waves 4-7 MFMAs first
+      if (a.part && (a.tune & 524288) && a.stem_in == STEM_IN_NCHW3) {  // one barrier, waves 4-7 MFMAs first
         hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3, 1>), gd, bd, 0, st, a, ntiles);
         break;
       }
-      if (a.part && !(a.tune & 262144)) {  // round 3b: one barrier per tile (A/B: tune bit 262144)
+      if (a.part && (a.tune & 262144)) {  // round 3b: one barrier per tile (opt-in until measured)
         switch (a.stem_in) {
           case STEM_IN_NCHW3:
             hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3>), gd, bd, 0, st, a, ntiles);
