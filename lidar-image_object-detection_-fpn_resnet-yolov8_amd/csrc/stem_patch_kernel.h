@@ -434,31 +434,48 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool2_kernel(const ConvArgs
   const int tw_n = a.OW / TW, tiles_per_frame = (a.OH / TH) * tw_n;
   const int PHo = a.OH >> 1, PWo = a.OW >> 1;
 
+  // Patch fetch. NHWC4: thread p loads patch pixels p, p + 512, p + 1024 (one float4 each).
+  // NCHW3 (and flipped): item p < 370 = (patch row p / 10, column group p % 10) loads columns
+  // 32 tw - 4 + 4 q .. + 3 of that row from each of the three planes as one aligned float4 (W % 4
+  // == 0: a group lies wholly inside or wholly outside the image), i.e. patch columns 4 q - 1 ..
+  // 4 q + 2 (column -1 is dropped): 3 loads per item instead of 3 per pixel.
+  constexpr bool VEC = IN != STEM_IN_NHWC4;
+  constexpr int NG = (PW + 1 + 3) / 4;  // column groups per patch row: 10
+  static_assert(!VEC || PH * NG <= NT, "one item per thread");
   x6_f32x4 R0[PF], R1[PF];
   auto fetch = [&](int tile, x6_f32x4 (&pf)[PF]) {
     const int b = tile / tiles_per_frame, tl = tile - b * tiles_per_frame;
     const int th = tl / tw_n, tw = tl - th * tw_n;
     const int iy0 = 2 * TH * th - 3, ix0 = 2 * TW * tw - 3;
     const size_t hw = (size_t)g.H * g.W;
+    if constexpr (VEC) {
+      const int py = tid / NG, q = tid - py * NG;
+      const int iy = iy0 + py, ixg = ix0 - 1 + 4 * q;
+      x6_f32x4 z = {0.f, 0.f, 0.f, 0.f};
+      pf[0] = z;
+      pf[1] = z;
+      pf[2] = z;
+      if (py < PH && (unsigned)iy < (unsigned)g.H && (unsigned)ixg < (unsigned)g.W) {
+        const int sy = IN == STEM_IN_NCHW3_FLIP ? g.H - 1 - iy : iy;
+        const int sx = IN == STEM_IN_NCHW3_FLIP ? g.W - 4 - ixg : ixg;
+        const float* x = g.x + (size_t)b * 3 * hw + (size_t)sy * g.W + sx;
 #pragma unroll
-    for (int j = 0; j < PF; ++j) {
-      const int p = tid + j * NT;
-      const int py = p / PW, px = p - py * PW;
-      const int iy = iy0 + py, ix = ix0 + px;
-      x6_f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (p < PIX && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W) {
-        if constexpr (IN == STEM_IN_NHWC4) {
-          v = reinterpret_cast<const x6_f32x4*>(g.x)[(size_t)b * hw + iy * g.W + ix];
-        } else {
-          const int sy = IN == STEM_IN_NCHW3_FLIP ? g.H - 1 - iy : iy;
-          const int sx = IN == STEM_IN_NCHW3_FLIP ? g.W - 1 - ix : ix;
-          const float* x = g.x + (size_t)b * 3 * hw + (size_t)sy * g.W + sx;
-          v[0] = x[0];
-          v[1] = x[hw];
-          v[2] = x[2 * hw];
+        for (int c = 0; c < 3; ++c) {
+          const x6_f32x4 v = *reinterpret_cast<const x6_f32x4*>(x + c * hw);
+          pf[c] = IN == STEM_IN_NCHW3_FLIP ? x6_f32x4{v[3], v[2], v[1], v[0]} : v;
         }
       }
-      pf[j] = v;
+    } else {
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const int p = tid + j * NT;
+        const int py = p / PW, px = p - py * PW;
+        const int iy = iy0 + py, ix = ix0 + px;
+        x6_f32x4 v = {0.f, 0.f, 0.f, 0.f};
+        if (p < PIX && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
+          v = reinterpret_cast<const x6_f32x4*>(g.x)[(size_t)b * hw + iy * g.W + ix];
+        pf[j] = v;
+      }
     }
   };
   auto patch_max = [&](const x6_f32x4 (&pf)[PF], float* dst) {
@@ -477,14 +494,30 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool2_kernel(const ConvArgs
     for (int w = 1; w < NW; ++w) tmax = fmaxf(tmax, wm[w]);
     float ainv;
     const float s = amax_scale_bits(__float_as_uint(tmax), ainv);
+    if constexpr (VEC) {
+      const int py = tid / NG, q = tid - py * NG;
+      if (py < PH) {
 #pragma unroll
-    for (int j = 0; j < PF; ++j) {
-      const int p = tid + j * NT;
-      if (p < PIX) {
-        f16x4_t hi, lo;
-        split2h(pf[j], s, hi, lo);
-        *reinterpret_cast<f16x4_t*>(SU + p * 8) = hi;
-        *reinterpret_cast<f16x4_t*>(SU + PATCH_TERM + p * 8) = lo;
+        for (int e = 0; e < 4; ++e) {
+          const int px = 4 * q - 1 + e;
+          if (px >= 0 && px < PW) {
+            f16x4_t hi, lo;
+            split2h(x6_f32x4{pf[0][e], pf[1][e], pf[2][e], 0.f}, s, hi, lo);
+            *reinterpret_cast<f16x4_t*>(SU + (py * PW + px) * 8) = hi;
+            *reinterpret_cast<f16x4_t*>(SU + PATCH_TERM + (py * PW + px) * 8) = lo;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < PF; ++j) {
+        const int p = tid + j * NT;
+        if (p < PIX) {
+          f16x4_t hi, lo;
+          split2h(pf[j], s, hi, lo);
+          *reinterpret_cast<f16x4_t*>(SU + p * 8) = hi;
+          *reinterpret_cast<f16x4_t*>(SU + PATCH_TERM + p * 8) = lo;
+        }
       }
     }
     return ainv;
@@ -556,22 +589,19 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool2_kernel(const ConvArgs
     }
   };
 
-  int k = 0;
-  for (int tile = t0; tile < ntiles; tile += G, ++k) {
-    const int par = k & 1;
+  // one tile; PAR = its parity (patch buffer, exchange buffer, maxima slots). Rs holds the next
+  // tile's patch (split now, then refilled with the patch three tiles ahead), Rm the patch two
+  // tiles ahead (its max reduced at the end). Compile-time parity keeps both sets in registers.
+  auto body = [&](auto par_c, int tile, x6_f32x4 (&Rs)[PF], x6_f32x4 (&Rm)[PF]) {
+    constexpr int par = decltype(par_c)::value;
     unsigned char* SUc = SU0 + par * 2 * PATCH_TERM;
     unsigned char* SUn = SU0 + (par ^ 1) * 2 * PATCH_TERM;
     const bool has_next = tile + G < ntiles;
     float ainv_next = 0.f;
     auto prep_next = [&]() {  // the next tile's patch into the other buffer; refill its registers
       if (!has_next) return;
-      if (par == 0) {
-        ainv_next = split_patch(WMX + NW, R1, SUn);
-        if (tile + 3 * G < ntiles) fetch(tile + 3 * G, R1);
-      } else {
-        ainv_next = split_patch(WMX, R0, SUn);
-        if (tile + 3 * G < ntiles) fetch(tile + 3 * G, R0);
-      }
+      ainv_next = split_patch(WMX + (par ^ 1) * NW, Rs, SUn);
+      if (tile + 3 * G < ntiles) fetch(tile + 3 * G, Rs);
     };
     const bool late = (ABL & 1) != 0 && wave >= NW / 2;
     if (!late) {
@@ -644,10 +674,21 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool2_kernel(const ConvArgs
     for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
     if (lane == 0) TMX[par * NW + wave] = mx;
     // the max of the patch two tiles ahead (its registers were refilled during the previous tile)
-    if (tile + 2 * G < ntiles) patch_max(par == 0 ? R0 : R1, WMX + par * NW);
+    if (tile + 2 * G < ntiles) patch_max(Rm, WMX + par * NW);
     prev_tile = tile;
     ainv_cur = ainv_next;
     __syncthreads();
+  };
+  int k = 0;
+  for (int tile = t0;;) {
+    if (tile >= ntiles) break;
+    body(std::integral_constant<int, 0>(), tile, R1, R0);
+    tile += G;
+    ++k;
+    if (tile >= ntiles) break;
+    body(std::integral_constant<int, 1>(), tile, R0, R1);
+    tile += G;
+    ++k;
   }
   finish_prev((k - 1) & 1);
 }
@@ -690,19 +731,25 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
     case 16: hipLaunchKernelGGL((stem_patch_pool_kernel<16, NC3>), gd, bd, 0, st, a, ntiles); break;
     case 64: hipLaunchKernelGGL((stem_patch_pool_kernel<64, NC3>), gd, bd, 0, st, a, ntiles); break;
     default:
-      if (a.part && (a.tune & 524288) && a.stem_in == STEM_IN_NCHW3) {  // one barrier, waves 4-7 MFMAs first
-        hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3, 1>), gd, bd, 0, st, a, ntiles);
-        break;
-      }
-      if (a.part && (a.tune & 262144)) {  // round 3b: one barrier per tile (opt-in until measured)
+      // default: the one-barrier kernel with waves 4-7 issuing their MFMAs first (it reads NCHW3
+      // planes as aligned float4 column groups); tune bit 262144: one barrier, all waves in the
+      // same order; bit 524288: the three-barrier kernel (round 3a)
+      const bool al16 = (reinterpret_cast<uintptr_t>(a.seg[0].x) & 15) == 0;
+      if (a.part && !(a.tune & 524288) && (al16 || a.stem_in == STEM_IN_NHWC4)) {
+        const bool same = (a.tune & 262144) != 0;
         switch (a.stem_in) {
           case STEM_IN_NCHW3:
-            hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3>), gd, bd, 0, st, a, ntiles);
+            if (same) hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3, 0>), gd, bd, 0, st, a, ntiles);
+            else hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3, 1>), gd, bd, 0, st, a, ntiles);
             break;
           case STEM_IN_NCHW3_FLIP:
-            hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3_FLIP>), gd, bd, 0, st, a, ntiles);
+            if (same) hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3_FLIP, 0>), gd, bd, 0, st, a, ntiles);
+            else hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3_FLIP, 1>), gd, bd, 0, st, a, ntiles);
             break;
-          default: hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NHWC4>), gd, bd, 0, st, a, ntiles); break;
+          default:
+            if (same) hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NHWC4, 0>), gd, bd, 0, st, a, ntiles);
+            else hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NHWC4, 1>), gd, bd, 0, st, a, ntiles);
+            break;
         }
         break;
       }
