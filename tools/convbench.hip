@@ -270,10 +270,7 @@ int main(int argc, char** argv) {
   };
   // round 2: conv_r3_kernel (A in registers) against the round-1 defaults (first entry of each)
   std::vector<Cand> n64 = {
-      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDR(256, 64, 32, EPI_STD, 2, 2, 555264, 1),
-      CANDR(128, 64, 32, EPI_STD, 4, 2, 555264, 1), CANDR(256, 64, 64, EPI_STD, 2, 2, 555264, 1),
-      CANDR(128, 64, 32, EPI_STD, 4, 2, 547072, 1), CANDW(32, 8, 18, 2, 0), CANDW(32, 8, 18, 3, 0),
-      CANDW(16, 8, 18, 2, 0),
+      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDR(128, 64, 32, EPI_STD, 4, 2, 555264, 1), CANDW(32, 8, 18, 2, 0),
   };
   std::vector<Cand> stem = {
       CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
@@ -285,8 +282,7 @@ int main(int argc, char** argv) {
   };
   std::vector<Cand> heads = {
       CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 2, 620804, 1),
-      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1670404, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1),
-      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 3766532, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
