@@ -171,10 +171,14 @@ int sfa_model_get_math(const sfa_model* model);
  *   SFA_OPT_FPN_COMMUTE      (SFA_FPN_COMMUTE)      bit mask of FPN levels run commuted (7)
  *   SFA_OPT_FPN3_SIDE        (SFA_FPN3_SIDE)        1: second side stream (re-creates streams)
  *   SFA_OPT_STEM_ABL         (SFA_STEM_ABL)         patch-stem timing ablations (wrong results)
+ *   SFA_OPT_HEADS_GROUPED    (SFA_HEADS_GROUPED)    the three levels' heads as ONE launch after the
+ *                                                   FPN (fp16x3; bit-identical): 1 always, 0 never
+ *                                                   (default), 2 when the model has no side stream
  */
 enum sfa_model_option {
   SFA_OPT_CONV_TUNE = 0, SFA_OPT_STEM_PATCH = 1, SFA_OPT_STEM_POOL_FUSION = 2,
-  SFA_OPT_STEM_PATCH_ATOMIC = 3, SFA_OPT_FPN_COMMUTE = 4, SFA_OPT_FPN3_SIDE = 5, SFA_OPT_STEM_ABL = 6
+  SFA_OPT_STEM_PATCH_ATOMIC = 3, SFA_OPT_FPN_COMMUTE = 4, SFA_OPT_FPN3_SIDE = 5, SFA_OPT_STEM_ABL = 6,
+  SFA_OPT_HEADS_GROUPED = 7
 };
 int sfa_model_set_option(sfa_model* model, int key, int value);
 int sfa_model_get_option(const sfa_model* model, int key, int* value);
@@ -185,7 +189,8 @@ int sfa_model_get_option(const sfa_model* model, int key, int* value);
  * that launches it; SFA_PROBE_SERIAL: all launches stay on the caller's stream (no
  * side streams), so each head launch has the chip to itself.  sfa_model_probe_times
  * waits for the last probed forward's events and returns the launch durations of head
- * levels 0 .. n-1 in ms.  flags = 0 turns the probe off. */
+ * levels 0 .. n-1 in ms (grouped heads, SFA_OPT_HEADS_GROUPED: the one launch's duration in
+ * entry 0, zeros after it).  flags = 0 turns the probe off. */
 enum sfa_probe_flags { SFA_PROBE_HEADS = 1, SFA_PROBE_SERIAL = 2 };
 int sfa_model_set_probe(sfa_model* model, int flags);
 int sfa_model_probe_times(const sfa_model* model, float* ms, int n);

@@ -300,6 +300,18 @@ int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t st) {
   return launch_conv_cfg<64, 64, 32, 32, 16, EPI_STD, 4>(a, st);
 }
 
+// The three KFPN levels' heads in one launch (conv_r3_group_kernel: longest K first, so the
+// per-level launches' partial last rounds of tiles become one short tail). fp16x3 and the
+// default head kernel only; SFA_E_UNSUPPORTED otherwise (the caller launches per level).
+int launch_conv_heads_group(const ConvArgs* lv, int n, int math, hipStream_t st) {
+  if (math != SFA_MATH_FP16X3 || n != 3) return SFA_E_UNSUPPORTED;
+  for (int i = 0; i < n; ++i) {
+    if (!lv[i].wh || !lv[i].winv || lv[i].N != 320 || lv[i].tune != lv[0].tune) return SFA_E_UNSUPPORTED;
+  }
+  if (lv[0].tune & (4 | 64 | 256 | 65536 | 131072)) return SFA_E_UNSUPPORTED;  // per-level A/B head kernels
+  return launch_conv_r3_group_cfg<256, 320, 32, 1, 3, R3_HEAD_STAG>(lv, n, st);
+}
+
 int launch_stem_patch(const ConvArgs& a, hipStream_t st) { return launch_stem_patch_pool(a, st); }
 
 }  // namespace sfa

@@ -440,8 +440,10 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
 // stages. The delayed half reads the next tile's first W blocks ahead across its tile boundary
 // (that tile was published by the barrier before); the leading half reads them after its
 // barrier. Same products in the same order: bit-identical to the unstaggered loop.
+// The kernel body for output tile (and split-K slice) lbid; conv_r3_kernel maps blockIdx to lbid
+// with xcd_remap, conv_r3_group_kernel (grouped head launch) per level.
 template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int NSEG, int ABL = 0>
-__global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const ConvArgs a) {
+__device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   static_assert(NSTAGE == 2 || NSTAGE == 3, "W ring depth");
   constexpr bool STAG = (ABL & 1048576) != 0;
   static_assert(!STAG || (NSTAGE == 3 && (ABL & 256) != 0 && (ABL & 2048) != 0 && (ABL & (8 | 16 | 32 | 64 | 128 | 512)) == 0),
@@ -469,7 +471,6 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   const int n_tiles = a.N / BN;
   const int m_tiles = (a.M + BM - 1) / BM;
   const int nsplit = a.ksplit > 1 ? a.ksplit : 1;
-  int lbid = xcd_remap(blockIdx.x, gridDim.x);
   const int kz = lbid / (m_tiles * n_tiles);  // split-K slice of this block
   lbid -= kz * (m_tiles * n_tiles);
   const int mt = lbid / n_tiles, nt = lbid - mt * n_tiles;
@@ -935,8 +936,37 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   }
 }
 
-template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int ABL = 0>
-inline int launch_conv_r3_cfg(const ConvArgs& a, hipStream_t st) {
+template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int NSEG, int ABL = 0>
+__global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const ConvArgs a) {
+  conv_r3_body<BM, BN, WM, EPI, OCC, NSTAGE, NSEG, ABL>(a, xcd_remap(blockIdx.x, gridDim.x));
+}
+
+// Grouped head launch: the three KFPN levels' fused head convs (EPI_HEAD, one segment, no
+// split-K) in ONE grid. Per-level launches end in a partial last round of tiles: level 0's 361
+// tiles of 72 K-tiles each fill 256 CUs 1.41 times (the second round runs 105 tiles while 151
+// CUs idle), levels 1 / 2 (1,444 tiles of 36 / 18 K-tiles) 5.64 times. Here blocks
+// [0, start1) are level a0's tiles, [start1, start2) a1's, [start2, grid) a2's, the levels
+// ordered by K (longest first: the hardware dispatches blocks in order, so the long tiles start
+// first and the short ones fill the end — longest-processing-time-first list scheduling); each
+// range starts at a multiple of 8, so blockIdx % 8 is still the XCD and xcd_remap within the
+// level keeps an XCD on contiguous tiles. Padding blocks return at once. Every tile computes
+// exactly what conv_r3_kernel computes for it: bit-identical to the per-level launches.
+template <int BM, int BN, int WM, int OCC, int NSTAGE, int ABL>
+__global__ void __launch_bounds__((BM / WM) * 64, OCC)
+    conv_r3_group_kernel(const ConvArgs a0, const ConvArgs a1, const ConvArgs a2, int start1, int start2) {
+  const int b = blockIdx.x;
+  const int lvl = b < start1 ? 0 : (b < start2 ? 1 : 2);
+  const int first = lvl == 0 ? 0 : (lvl == 1 ? start1 : start2);
+  const int end = lvl == 0 ? start1 : (lvl == 1 ? start2 : (int)gridDim.x);
+  const ConvArgs& a = lvl == 0 ? a0 : (lvl == 1 ? a1 : a2);
+  const int lb = xcd_remap(b - first, end - first);
+  if (lb >= ((a.M + BM - 1) / BM) * (a.N / BN)) return;  // padding block (uniform)
+  conv_r3_body<BM, BN, WM, EPI_HEAD, OCC, NSTAGE, 1, ABL>(a, lb);
+}
+
+// Launch-time checks of one conv_r3 launch (the kernel never bounds-checks these).
+template <int BM, int BN, int EPI, int ABL>
+inline int conv_r3_check(const ConvArgs& a) {
   if (!a.wh || !a.winv || a.Kpad % 32 != 0 || (a.nseg == 2 && a.kseg1 % 32 != 0) || a.N % BN != 0 ||
       (a.res_up && ((ABL & 32768) == 0 || (ABL & 2048) == 0 || a.res || a.nseg != 1))) {
     set_error("conv_r3: K/N not aligned to the tile, no split weights or an upsampled residual (Kpad=%d kseg1=%d N=%d)", a.Kpad,
@@ -973,6 +1003,14 @@ inline int launch_conv_r3_cfg(const ConvArgs& a, hipStream_t st) {
     set_error("conv_r3: split-K %d unsupported here (Kpad=%d N=%d)", ks, a.Kpad, a.N);
     return SFA_E_UNSUPPORTED;
   }
+  return SFA_OK;
+}
+
+template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int ABL = 0>
+inline int launch_conv_r3_cfg(const ConvArgs& a, hipStream_t st) {
+  const int crc = conv_r3_check<BM, BN, EPI, ABL>(a);
+  if (crc != SFA_OK) return crc;
+  const int ks = a.ksplit > 1 ? a.ksplit : 1;
   const long long nblocks = (long long)ceil_div(a.M, BM) * (a.N / BN) * ks;
   if (nblocks <= 0 || nblocks > 0x7fffffffll) {
     set_error("conv_r3: bad grid (M=%d N=%d)", a.M, a.N);
@@ -990,6 +1028,39 @@ inline int launch_conv_r3_cfg(const ConvArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((nel + 1023) / 1024)), dim3(256), 0, st, a);
     SFA_LAUNCH_CHECK();
   }
+  return SFA_OK;
+}
+
+// The grouped head launch (conv_r3_group_kernel) over n = 3 levels: one segment each, no
+// split-K, EPI_HEAD; the levels are ordered by K, longest first (stable).
+template <int BM, int BN, int WM, int OCC, int NSTAGE, int ABL>
+inline int launch_conv_r3_group_cfg(const ConvArgs* lv, int n, hipStream_t st) {
+  if (n != 3) {
+    set_error("conv_r3 group: %d levels (3 expected)", n);
+    return SFA_E_UNSUPPORTED;
+  }
+  int ord[3] = {0, 1, 2};
+  for (int i = 1; i < 3; ++i)
+    for (int j = i; j > 0 && lv[ord[j]].Kpad > lv[ord[j - 1]].Kpad; --j) std::swap(ord[j], ord[j - 1]);
+  long long start[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 3; ++i) {
+    const ConvArgs& a = lv[ord[i]];
+    const int crc = conv_r3_check<BM, BN, EPI_HEAD, ABL>(a);
+    if (crc != SFA_OK) return crc;
+    if (a.nseg != 1 || a.ksplit > 1) {
+      set_error("conv_r3 group: level %d is not a one-segment, unsplit conv", ord[i]);
+      return SFA_E_UNSUPPORTED;
+    }
+    const long long tiles = (long long)ceil_div(a.M, BM) * (a.N / BN);
+    start[i + 1] = start[i] + (tiles + 7) / 8 * 8;
+  }
+  if (start[3] <= 0 || start[3] > 0x7fffffffll) {
+    set_error("conv_r3 group: bad grid");
+    return SFA_E_INVALID;
+  }
+  hipLaunchKernelGGL((conv_r3_group_kernel<BM, BN, WM, OCC, NSTAGE, ABL>), dim3((unsigned)start[3]),
+                     dim3((BM / WM) * 64), 0, st, lv[ord[0]], lv[ord[1]], lv[ord[2]], (int)start[1], (int)start[2]);
+  SFA_LAUNCH_CHECK();
   return SFA_OK;
 }
 

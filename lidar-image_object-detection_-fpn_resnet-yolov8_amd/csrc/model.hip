@@ -307,9 +307,17 @@ struct sfa_model {
   // keeps every launch on the caller's stream so each head launch has the chip to itself.
   int probe = 0;
   hipEvent_t probe_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  bool probe_grouped = false;  // the last probed forward's heads ran as one grouped launch (events 0, 1)
   // kernel-choice options (sfa_model_set_option): conv tune bits, patch-stem ablation
   int tune = 0;
   int stem_abl = 0;
+  // heads as ONE launch of the three levels after the FPN (conv_r3_group_kernel): 1 always,
+  // 0 (default) never: one launch per level, 2 when the model has no side stream. Serially the
+  // grouped launch takes 7 % off the three per-level launches (their partial last rounds of
+  // tiles become one short tail), but with two steps in flight the other step's kernels fill
+  // those tails anyway: headline -0.8 %, stream workload -1.6 %, fusion +-0
+  // (profiles/r03n_ab_heads_grouped.txt) — kept for single-stream, one-step-at-a-time callers
+  int heads_grouped = 0;
 };
 
 // A conv's arguments with the model's kernel-choice options (ConvArgs::tune / stem_abl).
@@ -498,6 +506,7 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   if (const char* e = getenv("SFA_STEM_PATCH_ATOMIC")) m->stem_atomic = strcmp(e, "0") != 0;
   if (const char* e = getenv("SFA_FPN_COMMUTE")) m->fpn_commute = atoi(e) & 7;
   if (const char* e = getenv("SFA_FPN3_SIDE")) m->fpn3_side = strcmp(e, "0") != 0;
+  if (const char* e = getenv("SFA_HEADS_GROUPED")) m->heads_grouped = std::min(std::max(atoi(e), 0), 2);
   bool side_streams = true;  // env SFA_SIDE_STREAMS=0: every launch on the caller's stream (A/B)
   if (const char* e = getenv("SFA_SIDE_STREAMS")) side_streams = strcmp(e, "0") != 0;
   if (side_streams) make_side_streams(m);
@@ -553,6 +562,10 @@ extern "C" int sfa_model_set_option(sfa_model* model, int key, int value) {
       }
       break;
     case SFA_OPT_STEM_ABL: model->stem_abl = value; break;
+    case SFA_OPT_HEADS_GROUPED:
+      SFA_CHECK_ARG(value >= 0 && value <= 2, "set_option: HEADS_GROUPED %d not in 0..2", value);
+      model->heads_grouped = value;
+      break;
     default: set_error("set_option: unknown key %d", key); return SFA_E_INVALID;
   }
   return SFA_OK;
@@ -568,6 +581,7 @@ extern "C" int sfa_model_get_option(const sfa_model* model, int key, int* value)
     case SFA_OPT_FPN_COMMUTE: *value = model->fpn_commute; break;
     case SFA_OPT_FPN3_SIDE: *value = model->fpn3_side; break;
     case SFA_OPT_STEM_ABL: *value = model->stem_abl; break;
+    case SFA_OPT_HEADS_GROUPED: *value = model->heads_grouped; break;
     default: set_error("get_option: unknown key %d", key); return SFA_E_INVALID;
   }
   return SFA_OK;
@@ -597,6 +611,10 @@ extern "C" int sfa_model_probe_times(const sfa_model* model, float* ms, int n) {
   SFA_CHECK_ARG(model && ms && n >= 0 && n <= 3, "probe_times: bad arguments");
   SFA_CHECK_ARG(model->probe & SFA_PROBE_HEADS, "probe_times: probe not enabled");
   for (int f = 0; f < n; ++f) {
+    if (model->probe_grouped && f > 0) {  // one grouped launch: its duration is level 0's entry
+      ms[f] = 0.f;
+      continue;
+    }
     SFA_HIP_TRY(hipEventSynchronize(model->probe_ev[2 * f + 1]));
     SFA_HIP_TRY(hipEventElapsedTime(&ms[f], model->probe_ev[2 * f], model->probe_ev[2 * f + 1]));
   }
@@ -915,7 +933,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   const float* lin[3] = {F(bf.up2), F(bf.up3), F(bf.up4)};
   const int lh[3] = {H8, H4, H4}, lw[3] = {W8, W4, W4};
   float* lout[3] = {F(bf.L0), F(bf.L1), F(bf.L2)};
-  auto launch_head = [&](int f, hipStream_t hs) -> int {
+  auto head_args = [&](int f) -> ConvArgs {
     const PHeads& hp = p.heads[f];
     ConvArgs a;
     memset(&a, 0, sizeof a);
@@ -940,22 +958,48 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       a.hoff[j] = hoff[j];
     }
     a.hout = lout[f];
+    return tuned(a, m);
+  };
+  auto probing = [&](hipStream_t hs) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    const bool probe = (m->probe & SFA_PROBE_HEADS) && hipStreamIsCapturing(hs, &cap) == hipSuccess &&
-                       cap == hipStreamCaptureStatusNone;
+    return (m->probe & SFA_PROBE_HEADS) && hipStreamIsCapturing(hs, &cap) == hipSuccess &&
+           cap == hipStreamCaptureStatusNone;
+  };
+  auto launch_head = [&](int f, hipStream_t hs) -> int {
+    const bool probe = probing(hs);
     if (probe) SFA_HIP_TRY(hipEventRecord(m->probe_ev[2 * f], hs));
-    SFA_RC(launch_conv(tuned(a, m), EPI_HEAD, m->math, hs));
+    SFA_RC(launch_conv(head_args(f), EPI_HEAD, m->math, hs));
     if (probe) SFA_HIP_TRY(hipEventRecord(m->probe_ev[2 * f + 1], hs));
+    if (probe) const_cast<sfa_model*>(m)->probe_grouped = false;
     return SFA_OK;
   };
+  // all three levels in one launch (SFA_OPT_HEADS_GROUPED), or per level when the math mode /
+  // A/B head kernel has no grouped form
+  auto launch_heads_grouped = [&](hipStream_t hs) -> int {
+    const ConvArgs lv[3] = {head_args(0), head_args(1), head_args(2)};
+    const bool probe = probing(hs);
+    if (probe) SFA_HIP_TRY(hipEventRecord(m->probe_ev[0], hs));
+    const int rc = launch_conv_heads_group(lv, 3, m->math, hs);
+    if (rc == SFA_E_UNSUPPORTED) {
+      SFA_RC(launch_head(0, hs));
+      SFA_RC(launch_head(1, hs));
+      return launch_head(2, hs);
+    }
+    SFA_RC(rc);
+    if (probe) SFA_HIP_TRY(hipEventRecord(m->probe_ev[1], hs));
+    if (probe) const_cast<sfa_model*>(m)->probe_grouped = true;
+    return SFA_OK;
+  };
+  // (m->side is read under fork_mu below, as the overlap decision)
   // level 0 needs only up_level2: fork it onto the side stream (graph capture follows
   // the event edges), join before apply_kfpn
   // m->side / m->side2 are read under fork_mu: sfa_model_set_side_streams destroys them under
   // the same lock, so a concurrent call cannot pull a stream out from under this forward
   std::unique_lock<std::mutex> fork_lock(const_cast<sfa_model*>(m)->fork_mu);
   int sdev = -1;
-  const bool overlap = m->side && !(m->probe & SFA_PROBE_SERIAL) && hipStreamGetDevice(st, &sdev) == hipSuccess &&
-                       sdev == m->device;
+  const bool grouped = m->heads_grouped == 1 || (m->heads_grouped == 2 && !m->side);
+  const bool overlap = m->side && !grouped && !(m->probe & SFA_PROBE_SERIAL) &&
+                       hipStreamGetDevice(st, &sdev) == hipSuccess && sdev == m->device;
   const bool side2_on = overlap && m->side2 && m->fpn3_side;
   if (overlap) {
     SFA_HIP_TRY(hipEventRecord(m->fork, st));
@@ -968,7 +1012,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   auto forked = [&]() -> int {
   if (overlap) {
     SFA_RC(launch_head(0, m->side));
-  } else {
+  } else if (!grouped) {
     SFA_RC(launch_head(0, st));
   }
   if (commute_at(1)) {
@@ -1010,6 +1054,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     return SFA_OK;
   }
   SFA_RC(fpn3(st));
+  if (grouped) return launch_heads_grouped(st);
   // level 2 (needs up_level4, just written) on the side stream after level 0, level 1 here:
   // the two 1,444-tile launches run side by side, so neither one's last partial wave of tiles
   // leaves CUs idle

@@ -192,12 +192,15 @@ def test_argument_errors_before_any_launch():
         v = ctypes.c_int()
         defaults = {_lib.OPT_CONV_TUNE: 0, _lib.OPT_STEM_PATCH: 1, _lib.OPT_STEM_POOL_FUSION: 1,
                     _lib.OPT_STEM_PATCH_ATOMIC: 0, _lib.OPT_FPN_COMMUTE: 7, _lib.OPT_FPN3_SIDE: 0,
-                    _lib.OPT_STEM_ABL: 0}
+                    _lib.OPT_STEM_ABL: 0, _lib.OPT_HEADS_GROUPED: 0}
         for key, val in defaults.items():
             assert L.sfa_model_get_option(h, key, ctypes.byref(v)) == 0 and v.value == val, key
         assert L.sfa_model_set_option(h, _lib.OPT_CONV_TUNE, 28) == 0
         assert L.sfa_model_get_option(h, _lib.OPT_CONV_TUNE, ctypes.byref(v)) == 0 and v.value == 28
         assert L.sfa_model_set_option(h, _lib.OPT_FPN_COMMUTE, 9) == -1
+        assert L.sfa_model_set_option(h, _lib.OPT_HEADS_GROUPED, 3) == -1
+        assert L.sfa_model_set_option(h, _lib.OPT_HEADS_GROUPED, 1) == 0
+        assert L.sfa_model_get_option(h, _lib.OPT_HEADS_GROUPED, ctypes.byref(v)) == 0 and v.value == 1
         assert L.sfa_model_set_option(h, 99, 0) == -1 and b"unknown key" in L.sfa_last_error_string()
         assert L.sfa_model_get_option(h, 99, ctypes.byref(v)) == -1
         assert L.sfa_model_set_option(None, 0, 0) == -1

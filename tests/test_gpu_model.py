@@ -307,6 +307,53 @@ def test_heads_stagger_bit_identical(golden, gpu, hw):
         np.testing.assert_array_equal(outs[2][h], outs[0][h], err_msg=h)
 
 
+@pytest.mark.parametrize("hw", [(160, 192), (96, 96), (608, 608)])
+def test_heads_grouped_bit_identical(golden, gpu, hw):
+    """The three levels' heads as ONE launch (SFA_OPT_HEADS_GROUPED: conv_r3_group_kernel, level
+    tiles ordered by K, padding blocks) give the per-level launches' bits: every tile runs the
+    same body on the same arguments. With a per-level A/B head kernel (tune 65536) the grouped
+    option falls back to per-level launches, same bits again."""
+    x = torch.from_numpy(synthetic.synthetic_bev(2, hw[0], hw[1], seed=43)).to(gpu)
+    outs = []
+    for grouped, tune in ((0, 0), (1, 0), (1, 65536)):
+        model = make_model(golden, gpu)
+        eng = model._engine(gpu)
+        eng.set_option(_lib.OPT_CONV_TUNE, tune)
+        eng.set_option(_lib.OPT_HEADS_GROUPED, grouped)
+        eng.set_math(_math("fp16x3"))
+        with torch.no_grad():
+            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(outs[1][h], outs[0][h], err_msg=h)
+        np.testing.assert_array_equal(outs[2][h], outs[0][h], err_msg=h)
+
+
+def test_head_probe_grouped(golden, gpu):
+    """Probe with grouped heads: the one launch's duration in entry 0, zeros after it; results
+    unchanged; per-level probing again once the option is off."""
+    model = make_model(golden, gpu)
+    eng = model._engine(gpu)
+    eng.set_math(_math("fp16x3"))
+    x = torch.from_numpy(synthetic.synthetic_bev(3, 160, 192, seed=47)).to(gpu)
+    with torch.no_grad():
+        eng.set_option(_lib.OPT_HEADS_GROUPED, 0)
+        base = {h: v.cpu().numpy() for h, v in model(x).items()}
+        eng.set_option(_lib.OPT_HEADS_GROUPED, 1)
+        eng.set_probe(_lib.PROBE_HEADS | _lib.PROBE_SERIAL)
+        try:
+            probed = {h: v.cpu().numpy() for h, v in model(x).items()}
+            ms = eng.probe_times(3)
+            eng.set_option(_lib.OPT_HEADS_GROUPED, 0)
+            model(x)
+            ms_levels = eng.probe_times(3)
+        finally:
+            eng.set_probe(0)
+    assert ms[0] > 0 and ms[1] == 0 and ms[2] == 0, ms
+    assert all(t > 0 for t in ms_levels), ms_levels
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(base[h], probed[h], err_msg=h)
+
+
 @pytest.mark.parametrize("tune", [0, 28, 32, 256, 512, 65536])
 def test_batch_invariance_608(golden, gpu, tune):
     """At the full 608x608 size (every kernel path of the bench: r3 heads, strip convs, FPN skip
