@@ -60,17 +60,18 @@ const char* sfa_last_error_string(void);
  * scratch         device, sfa_bev_scratch_size(batch) bytes, ZERO on first use;
  *                 every call leaves it zeroed again (except the binned path's record
  *                 region, which is written before it is read).
- * Kernels: one pass bins every 1024 points of a frame by 8-row strips of the map into
+ * Kernels: one pass bins every 1024 points of a frame by 4-row strips of the map into
  * the pass block's own record region + a per-strip table, then one block per (frame, strip)
  * reduces its runs in LDS, while the batch's regions fit the scratch (~277 k points per
- * frame); SFA_BEV_FORCE_BINNED: round 2's count / scan / bin / strip form; otherwise (or with
+ * frame; SFA_BEV_STRIP8: 8-row strips); SFA_BEV_FORCE_BINNED: round 2's count / scan / bin / strip form; otherwise (or with
  * SFA_BEV_FORCE_ATOMIC) device-scope atomics on a per-cell scratch.  All give the same bits.
  */
 #define SFA_BEV_MAX_BATCH 64
 enum sfa_bev_layout { SFA_BEV_NCHW3_F32 = 0, SFA_BEV_NCHW3_F64 = 1, SFA_BEV_NHWC4_F32 = 2 };
 enum sfa_bev_flags {
   SFA_BEV_RAW = 0, SFA_BEV_PREFILTERED = 1, SFA_BEV_FLIP_HW = 2, SFA_BEV_FORCE_ATOMIC = 4,
-  SFA_BEV_FORCE_BINNED = 8  /* round 2's count / scan / bin / strip kernels (A/B) */
+  SFA_BEV_FORCE_BINNED = 8,  /* round 2's count / scan / bin / strip kernels (A/B) */
+  SFA_BEV_STRIP8 = 16        /* the one-pass path with 8-row strips (round 3a; A/B) */
 };
 
 size_t sfa_bev_scratch_size(int batch);

@@ -304,34 +304,55 @@ __global__ void __launch_bounds__(kStripThreads) bev_strip_kernel(const float4* 
 // [1024 j, 1024 j + 1024) and writes their records into ITS OWN 1024-record region, grouped by
 // strip (LDS histogram, exclusive scan, LDS slot per point), plus one word per strip into a
 // table: (first record of the strip in the region) | (count << 16). The strip pass for
-// (frame, strip) walks the frame's table column and reduces those runs in LDS. No count pass,
+// (frame, strip) reads the frame's table column and reduces those runs in LDS. No count pass,
 // no global scan, no global reservation atomics, and nothing to re-zero: the region and the
 // table are written before they are read. Region j of frame b starts at record
 // 1024 * (blk0[b] + j), blk0 = the exclusive sum of the frames' ceil(n / 1024) (host).
+// Strips of SR map rows: SR = 4 (default, round 3c) — 2,432-cell strips, 35 KiB of LDS per
+// 256-thread strip block, four blocks per CU — or SR = 8 (round 3a, SFA_BEV_STRIP8: 71 KiB,
+// two 512-thread blocks per CU). The table is stored strip-major (tab[strip][global region]),
+// so a strip block reads its column as one contiguous run, once. A record is 8 B: the top-point
+// key's z bits and (point index within its 1024-point region << 13 | cell within the strip) —
+// the region is the one the strip block found the record in, so the 64-bit key (z bits << 32 |
+// ~frame index) is rebuilt exactly (round 3a's 16-B records also carried the cell and the
+// intensity, which the strip pass takes from the top point).
 constexpr int kBlkPts = 1024;
 constexpr int kBlkThreads = 256;
 constexpr int kBlkPPT = kBlkPts / kBlkThreads;  // 4
 
+template <int SR>
+struct BlkGeom {
+  static constexpr int strips = kBevH / SR;         // 152 / 76
+  static constexpr int cells = SR * kBevW;          // 2,432 / 4,864
+  static constexpr int threads = SR == 8 ? 512 : 256;
+  static constexpr int max_regions = SR == 8 ? 2048 : 1024;  // regions of one frame a strip block indexes
+};
+
+constexpr int kBlkCellBits = 13;  // cell within a strip (< 4,864)
+static_assert(BlkGeom<8>::cells <= (1 << kBlkCellBits) && kBlkPts <= (1 << (32 - kBlkCellBits)), "record packing");
+
 struct BlkScratch {
-  uint4* rec;         // [total blocks][kBlkPts]
-  unsigned* tab;      // [total blocks][kStrips]: first | count << 16
+  uint2* rec;         // [total blocks][kBlkPts]: z bits, (index in region << 13) | cell in strip
+  unsigned* tab;      // [strips][total blocks]: first | count << 16
+  int nblk_total;     // total blocks (regions) of the batch: the table's row length
   int blk0[SFA_BEV_MAX_BATCH + 1];
 };
 
-template <bool RAW>
+template <bool RAW, int SR>
 __global__ void __launch_bounds__(kBlkThreads) bev_blk_bin_kernel(const float4* __restrict__ pts, BevArgs a,
                                                                   BlkScratch bs) {
-  __shared__ unsigned hist[kStrips], first[kStrips];
+  constexpr int NS = BlkGeom<SR>::strips, SC = BlkGeom<SR>::cells;
+  constexpr int P = (NS + 63) / 64;  // strips per lane of the scan
+  __shared__ unsigned hist[NS], first[NS];
   const int b = blockIdx.y, j = blockIdx.x;
   const int64_t s = a.start[b];
   const int64_t n = a.start[b + 1] - s;
   if ((int64_t)j * kBlkPts >= n) return;  // past this frame's points (the grid fits the largest)
-  for (int t = threadIdx.x; t < kStrips; t += kBlkThreads) hist[t] = 0u;
+  for (int t = threadIdx.x; t < NS; t += kBlkThreads) hist[t] = 0u;
   __syncthreads();
   int cell[kBlkPPT], strip[kBlkPPT];
   unsigned long long key[kBlkPPT];
   unsigned slot[kBlkPPT];
-  float inten[kBlkPPT];
   bool ok[kBlkPPT];
 #pragma unroll
   for (int q = 0; q < kBlkPPT; ++q) {
@@ -339,70 +360,78 @@ __global__ void __launch_bounds__(kBlkThreads) bev_blk_bin_kernel(const float4* 
     float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
     if (i < n) p = pts[s + i];
     ok[q] = i < n && bev_point_cell<RAW>(p, a, i, cell[q], key[q]);
-    inten[q] = p.w;
-    strip[q] = ok[q] ? cell[q] / kStripCells : 0;
+    strip[q] = ok[q] ? cell[q] / SC : 0;
     slot[q] = ok[q] ? atomicAdd(&hist[strip[q]], 1u) : 0u;
   }
   __syncthreads();
-  if (threadIdx.x < 64) {  // exclusive scan of the 76 strip counts (lane: bins 2 l, 2 l + 1)
+  if (threadIdx.x < 64) {  // exclusive scan of the strip counts (lane l: strips P l .. P l + P - 1)
     const int l = threadIdx.x;
-    const unsigned c0 = 2 * l < kStrips ? hist[2 * l] : 0u, c1 = 2 * l + 1 < kStrips ? hist[2 * l + 1] : 0u;
-    unsigned x = c0 + c1;
+    unsigned c[P], sum = 0u;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      c[q] = P * l + q < NS ? hist[P * l + q] : 0u;
+      sum += c[q];
+    }
+    unsigned x = sum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const unsigned y = __shfl_up(x, d, 64);
       if (l >= d) x += y;
     }
-    const unsigned e0 = x - c0 - c1;
-    if (2 * l < kStrips) first[2 * l] = e0;
-    if (2 * l + 1 < kStrips) first[2 * l + 1] = e0 + c0;
+    unsigned e = x - sum;
+#pragma unroll
+    for (int q = 0; q < P; ++q) {
+      if (P * l + q < NS) first[P * l + q] = e;
+      e += c[q];
+    }
   }
   __syncthreads();
   const size_t region = (size_t)(bs.blk0[b] + j);
-  for (int t = threadIdx.x; t < kStrips; t += kBlkThreads) bs.tab[region * kStrips + t] = first[t] | (hist[t] << 16);
-  uint4* rec = bs.rec + region * kBlkPts;
+  for (int t = threadIdx.x; t < NS; t += kBlkThreads)
+    bs.tab[(size_t)t * bs.nblk_total + region] = first[t] | (hist[t] << 16);
+  uint2* rec = bs.rec + region * kBlkPts;
 #pragma unroll
   for (int q = 0; q < kBlkPPT; ++q)
     if (ok[q])
-      rec[first[strip[q]] + slot[q]] = make_uint4((unsigned)(key[q] & 0xffffffffull), (unsigned)(key[q] >> 32),
-                                                  (unsigned)(cell[q] - strip[q] * kStripCells), __float_as_uint(inten[q]));
+      rec[first[strip[q]] + slot[q]] =
+          make_uint2((unsigned)(key[q] >> 32),
+                     ((unsigned)(q * kBlkThreads + threadIdx.x) << kBlkCellBits) | (unsigned)(cell[q] - strip[q] * SC));
 }
 
-constexpr int kBlkMaxRegions = 2048;  // regions of one frame the strip pass can index (2.1 M points)
-
 // One block per (frame, strip): the strip's records — runs in the bin pass's regions, located by
-// a scan of the strip's table column and a binary search over it — reduced in LDS (max key and
-// count per cell), then every cell of the strip written, the top points' intensities gathered
-// first so all those loads are in flight together. (Measured and not adopted: the intensity
-// taken from the records in a second pass over them, no random reads of the points — 144 vs
-// 170 MB per call, but 1,024-thread blocks with 90 KiB of LDS, 56 vs 46 us:
-// profiles/r03f_pmc_bev_blocked_v3_intensity_in_records.json.)
-template <int LAYOUT, bool FLIP>
-__global__ void __launch_bounds__(kStripThreads) bev_blk_strip_kernel(const float4* __restrict__ pts, BevArgs a,
-                                                                      BlkScratch bs, void* __restrict__ out) {
-  constexpr int NT = kStripThreads;
-  __shared__ unsigned long long skey[kStripCells];
-  __shared__ unsigned scnt[kStripCells];
-  __shared__ unsigned pre[kBlkMaxRegions + 1];  // this strip's records before region r
-  __shared__ unsigned short first[kBlkMaxRegions];
+// a scan of the strip's table column (read once, contiguous) and a binary search over it —
+// reduced in LDS (max key and count per cell), then every cell of the strip written, the top
+// points' intensities gathered first so all those loads are in flight together. (Measured and
+// not adopted: the intensity taken from the records in a second pass over them, no random reads
+// of the points — 144 vs 170 MB per call, but 1,024-thread blocks with 90 KiB of LDS, 56 vs 46
+// us: profiles/r03f_pmc_bev_blocked_v3_intensity_in_records.json.)
+template <int LAYOUT, bool FLIP, int SR>
+__global__ void __launch_bounds__(BlkGeom<SR>::threads) bev_blk_strip_kernel(const float4* __restrict__ pts, BevArgs a,
+                                                                             BlkScratch bs, void* __restrict__ out) {
+  constexpr int NT = BlkGeom<SR>::threads, SC = BlkGeom<SR>::cells, MAXR = BlkGeom<SR>::max_regions;
+  constexpr int RPT = MAXR / NT;  // table words per thread (at most)
+  __shared__ unsigned long long skey[SC];
+  __shared__ unsigned scnt[SC];
+  __shared__ unsigned pre[MAXR + 1];  // this strip's records before region r
+  __shared__ unsigned short first[MAXR];
   __shared__ unsigned wsum[NT / 64];
   const int strip = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
-  for (int c = tid; c < kStripCells; c += NT) {
+  for (int c = tid; c < SC; c += NT) {
     skey[c] = 0ull;
     scnt[c] = 0u;
   }
-  const int nblk = bs.blk0[b + 1] - bs.blk0[b];  // <= kBlkMaxRegions (checked at launch)
+  const int nblk = bs.blk0[b + 1] - bs.blk0[b];  // <= MAXR (checked at launch)
   const size_t reg0 = (size_t)bs.blk0[b];
+  const unsigned* col = bs.tab + (size_t)strip * bs.nblk_total + reg0;
   // exclusive scan of the regions' counts of this strip: thread t owns regions [t*per, t*per+per)
   const int per = (nblk + NT - 1) / NT;
+  unsigned wv[RPT];
   unsigned loc = 0;
-  for (int q = 0; q < per; ++q) {
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
     const int r = tid * per + q;
-    if (r < nblk) {
-      const unsigned w = bs.tab[(reg0 + r) * kStrips + strip];
-      first[r] = (unsigned short)(w & 0xffffu);
-      loc += w >> 16;
-    }
+    wv[q] = q < per && r < nblk ? col[r] : 0u;
+    loc += wv[q] >> 16;
   }
   unsigned x = loc;
 #pragma unroll
@@ -411,14 +440,16 @@ __global__ void __launch_bounds__(kStripThreads) bev_blk_strip_kernel(const floa
     if ((tid & 63) >= d) x += y;
   }
   if ((tid & 63) == 63) wsum[tid >> 6] = x;
-  __syncthreads();  // also: skey / scnt / first written
+  __syncthreads();  // also: skey / scnt written
   unsigned run = x - loc;
   for (int w = 0; w < (tid >> 6); ++w) run += wsum[w];
-  for (int q = 0; q < per; ++q) {
+#pragma unroll
+  for (int q = 0; q < RPT; ++q) {
     const int r = tid * per + q;
-    if (r < nblk) {
+    if (q < per && r < nblk) {
       pre[r] = run;
-      run += bs.tab[(reg0 + r) * kStrips + strip] >> 16;
+      first[r] = (unsigned short)(wv[q] & 0xffffu);
+      run += wv[q] >> 16;
     }
   }
   if (tid == NT - 1) {  // the total: every thread's count
@@ -431,7 +462,8 @@ __global__ void __launch_bounds__(kStripThreads) bev_blk_strip_kernel(const floa
   // every record of the strip, 4 per thread per round: region by binary search over pre, the 4
   // loads in flight together, then the LDS max / add
   for (unsigned base = 0; base < total; base += 4 * NT) {
-    uint4 e[4];
+    uint2 e[4];
+    int reg[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const unsigned idx = base + u * NT + tid;
@@ -440,29 +472,32 @@ __global__ void __launch_bounds__(kStripThreads) bev_blk_strip_kernel(const floa
         const int mid = (lo + hi + 1) >> 1;
         if (pre[mid] <= idx) lo = mid; else hi = mid - 1;
       }
-      e[u] = idx < total ? bs.rec[(reg0 + lo) * kBlkPts + first[lo] + (idx - pre[lo])] : make_uint4(0u, 0u, 0u, 0u);
+      reg[u] = lo;
+      e[u] = idx < total ? bs.rec[(reg0 + lo) * kBlkPts + first[lo] + (idx - pre[lo])] : make_uint2(0u, 0u);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u)
       if (base + u * NT + tid < total) {
-        atomicMax(&skey[e[u].z], ((unsigned long long)e[u].y << 32) | e[u].x);
-        atomicAdd(&scnt[e[u].z], 1u);
+        const unsigned c = e[u].y & ((1u << kBlkCellBits) - 1u);
+        const unsigned i = (unsigned)reg[u] * kBlkPts + (e[u].y >> kBlkCellBits);  // index within the frame
+        atomicMax(&skey[c], ((unsigned long long)e[u].x << 32) | (unsigned)~i);
+        atomicAdd(&scnt[c], 1u);
       }
   }
   __syncthreads();
   // every cell of the strip: the top points' intensities gathered first (all loads in flight),
   // then the three channels stored
-  constexpr int CPT = (kStripCells + NT - 1) / NT;
+  constexpr int CPT = (SC + NT - 1) / NT;
   float inten[CPT];
 #pragma unroll
   for (int q = 0; q < CPT; ++q) {
     const int c = tid + q * NT;
-    inten[q] = c < kStripCells ? bev_top_intensity(pts, a, b, scnt[c], skey[c]) : 0.f;
+    inten[q] = c < SC ? bev_top_intensity(pts, a, b, scnt[c], skey[c]) : 0.f;
   }
 #pragma unroll
   for (int q = 0; q < CPT; ++q) {
     const int c = tid + q * NT;
-    if (c < kStripCells) bev_store_cell_i<LAYOUT, FLIP>(a, b, strip * kStripCells + c, scnt[c], skey[c], inten[q], out);
+    if (c < SC) bev_store_cell_i<LAYOUT, FLIP>(a, b, strip * SC + c, scnt[c], skey[c], inten[q], out);
   }
 }
 
@@ -489,7 +524,8 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
                 SFA_BEV_MAX_BATCH);
   SFA_CHECK_ARG(frame_offsets && boundary && out && scratch, "bev: null argument");
   SFA_CHECK_ARG(out_layout >= 0 && out_layout <= 2, "bev: bad out_layout %d", out_layout);
-  SFA_CHECK_ARG((flags & ~(SFA_BEV_PREFILTERED | SFA_BEV_FLIP_HW | SFA_BEV_FORCE_ATOMIC | SFA_BEV_FORCE_BINNED)) == 0,
+  SFA_CHECK_ARG((flags & ~(SFA_BEV_PREFILTERED | SFA_BEV_FLIP_HW | SFA_BEV_FORCE_ATOMIC | SFA_BEV_FORCE_BINNED |
+                           SFA_BEV_STRIP8)) == 0,
                 "bev: bad flags %d", flags);
   const int flags_in = flags;
   const bool flip = (flags & SFA_BEV_FLIP_HW) != 0;
@@ -530,6 +566,9 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
   const float4* p4 = reinterpret_cast<const float4*>(points);
   // blocked-bin path (default) when the batch's regions and table fit the binned scratch
   {
+    const bool s8 = (flags_in & SFA_BEV_STRIP8) != 0;
+    const int nstrips = s8 ? BlkGeom<8>::strips : BlkGeom<4>::strips;
+    const int maxr = s8 ? BlkGeom<8>::max_regions : BlkGeom<4>::max_regions;
     BlkScratch bk;
     int64_t nblk_total = 0;
     for (int b = 0; b < batch; ++b) {
@@ -537,28 +576,37 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
       nblk_total += (frame_offsets[b + 1] - frame_offsets[b] + kBlkPts - 1) / kBlkPts;
     }
     bk.blk0[batch] = (int)nblk_total;
-    const size_t rec_bytes = align_up((size_t)nblk_total * kBlkPts * sizeof(uint4), 256);
-    const size_t tab_bytes = (size_t)nblk_total * kStrips * sizeof(unsigned);
+    bk.nblk_total = (int)nblk_total;
+    const size_t rec_bytes = align_up((size_t)nblk_total * kBlkPts * sizeof(uint2), 256);
+    const size_t tab_bytes = (size_t)nblk_total * nstrips * sizeof(unsigned);
     // after the binned path's (zero) counters, which it must not touch
     const size_t cnt_bytes = 3 * align_up((size_t)batch * kStrips * sizeof(unsigned), 256);
     int max_regions = 0;
     for (int b = 0; b < batch; ++b) max_regions = std::max(max_regions, bk.blk0[b + 1] - bk.blk0[b]);
-    if (!force_atomic && !(flags_in & SFA_BEV_FORCE_BINNED) && max_regions <= kBlkMaxRegions &&
+    if (!force_atomic && !(flags_in & SFA_BEV_FORCE_BINNED) && max_regions <= maxr &&
         cnt_bytes + rec_bytes + tab_bytes <= bev_atomic_bytes(batch)) {
       char* sb = reinterpret_cast<char*>(scratch) + bev_atomic_bytes(batch) + cnt_bytes;
-      bk.rec = reinterpret_cast<uint4*>(sb);
+      bk.rec = reinterpret_cast<uint2*>(sb);
       bk.tab = reinterpret_cast<unsigned*>(sb + rec_bytes);
       if (max_n > 0) {
         dim3 g1((unsigned)((max_n + kBlkPts - 1) / kBlkPts), batch);
-        if (flags == SFA_BEV_RAW)
-          hipLaunchKernelGGL(bev_blk_bin_kernel<true>, g1, dim3(kBlkThreads), 0, st, p4, a, bk);
-        else
-          hipLaunchKernelGGL(bev_blk_bin_kernel<false>, g1, dim3(kBlkThreads), 0, st, p4, a, bk);
+        if (flags == SFA_BEV_RAW) {
+          if (s8) hipLaunchKernelGGL((bev_blk_bin_kernel<true, 8>), g1, dim3(kBlkThreads), 0, st, p4, a, bk);
+          else hipLaunchKernelGGL((bev_blk_bin_kernel<true, 4>), g1, dim3(kBlkThreads), 0, st, p4, a, bk);
+        } else {
+          if (s8) hipLaunchKernelGGL((bev_blk_bin_kernel<false, 8>), g1, dim3(kBlkThreads), 0, st, p4, a, bk);
+          else hipLaunchKernelGGL((bev_blk_bin_kernel<false, 4>), g1, dim3(kBlkThreads), 0, st, p4, a, bk);
+        }
         SFA_LAUNCH_CHECK();
       }
-      dim3 g3(kStrips, batch);
-#define SFA_BEV_BLK(L, F) \
-  hipLaunchKernelGGL((bev_blk_strip_kernel<L, F>), g3, dim3(kStripThreads), 0, st, p4, a, bk, out)
+      dim3 g3(nstrips, batch);
+#define SFA_BEV_BLK(L, F)                                                                                    \
+  do {                                                                                                      \
+    if (s8)                                                                                                 \
+      hipLaunchKernelGGL((bev_blk_strip_kernel<L, F, 8>), g3, dim3(BlkGeom<8>::threads), 0, st, p4, a, bk, out); \
+    else                                                                                                    \
+      hipLaunchKernelGGL((bev_blk_strip_kernel<L, F, 4>), g3, dim3(BlkGeom<4>::threads), 0, st, p4, a, bk, out); \
+  } while (0)
       switch (out_layout) {
         case SFA_BEV_NCHW3_F32:
           if (flip) SFA_BEV_BLK(SFA_BEV_NCHW3_F32, true); else SFA_BEV_BLK(SFA_BEV_NCHW3_F32, false);

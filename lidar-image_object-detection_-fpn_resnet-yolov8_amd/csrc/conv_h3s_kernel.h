@@ -36,6 +36,8 @@ namespace sfa {
 // 16 = spread DMA: the k-step's W pieces (and the strip pieces, when due) are issued between the
 // MFMAs of column blocks 1, 2, .. (W first, then the strip: the counted waits are unchanged)
 // instead of in a burst right after the barrier.
+// 4096 = no W DMA inside the K loop (the first k-step's W is reused; ablation of the W staging
+// latency, results wrong).
 template <int BM, int BN, int WM, int EPI, int OCC, int ABL = 0>
 __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const ConvArgs a) {
   constexpr int NW = BM / WM, NT = NW * 64;
@@ -158,14 +160,17 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     }
   };
   auto load_w_piece = [&](int jj, int k0, unsigned char* S) {
+    if constexpr ((ABL & 4096) != 0) return;
     if (NB_REM == 0 || jj < NB - 1 || wave < NB_REM)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rsw, (__attribute__((address_space(3))) void*)(S + (wave + NW * jj) * 1024), 16,
           (unsigned)(boff[jj] + 2 * k0), 0, 0, 0);
   };
+  bool w_in_loop = false;  // ABL 4096: only the prologue's W DMA
   auto load_w = [&](int k0, unsigned char* S) {
 #pragma unroll
     for (int jj = 0; jj < NB; ++jj) {
+      if ((ABL & 4096) != 0 && w_in_loop) break;
       if (NB_REM == 0 || jj < NB - 1 || wave < NB_REM)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rsw, (__attribute__((address_space(3))) void*)(S + (wave + NW * jj) * 1024), 16,
@@ -308,6 +313,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
   unsigned char* const WB = smem + NSB * S_BYTES;
   load_strip(s0, smem);
   load_w(wk0(s0, 0), WB);
+  w_in_loop = true;
   for (int sl = 0; sl < nsl; ++sl) {
     const int s = s0 + sl;
     const bool last = sl + 1 == nsl;

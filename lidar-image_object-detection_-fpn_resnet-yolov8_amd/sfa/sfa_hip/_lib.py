@@ -23,7 +23,7 @@ SFA_OK = 0
 SFA_MAX_HEADS = 8
 SFA_BEV_MAX_BATCH = 64
 BEV_NCHW3_F32, BEV_NCHW3_F64, BEV_NHWC4_F32 = 0, 1, 2
-BEV_RAW, BEV_PREFILTERED, BEV_FLIP_HW, BEV_FORCE_ATOMIC, BEV_FORCE_BINNED = 0, 1, 2, 4, 8
+BEV_RAW, BEV_PREFILTERED, BEV_FLIP_HW, BEV_FORCE_ATOMIC, BEV_FORCE_BINNED, BEV_STRIP8 = 0, 1, 2, 4, 8, 16
 # sfa_model_set_option keys (include/sfa_hip.h sfa_model_option)
 (OPT_CONV_TUNE, OPT_STEM_PATCH, OPT_STEM_POOL_FUSION, OPT_STEM_PATCH_ATOMIC, OPT_FPN_COMMUTE,
  OPT_FPN3_SIDE, OPT_STEM_ABL, OPT_HEADS_GROUPED) = range(8)

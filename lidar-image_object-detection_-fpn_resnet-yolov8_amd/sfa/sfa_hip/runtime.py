@@ -237,13 +237,17 @@ class KfpnEngine:
 class BevVoxelizer:
     """sfa_bev_voxelize with its (self-cleaning) scratch kept resident."""
 
-    def __init__(self, device, max_batch: int = 16, force_atomic: bool = None):
+    def __init__(self, device, max_batch: int = 16, force_atomic: bool = None, strip8: bool = None):
         """force_atomic: the global-atomic kernels instead of the binned ones (same bits; A/B),
-        default from env SFA_BEV_ATOMIC read once here (flag SFA_BEV_FORCE_ATOMIC per call)."""
+        default from env SFA_BEV_ATOMIC read once here (flag SFA_BEV_FORCE_ATOMIC per call);
+        strip8: the one-pass path with 8-row strips (round 3a; A/B), env SFA_BEV_STRIP8."""
         self.device = torch.device(device)
         if force_atomic is None:
             force_atomic = os.environ.get("SFA_BEV_ATOMIC", "0") not in ("", "0")
+        if strip8 is None:
+            strip8 = os.environ.get("SFA_BEV_STRIP8", "0") not in ("", "0")
         self.force_atomic = bool(force_atomic)
+        self.strip8 = bool(strip8)
         self.max_batch = 0
         self.scratch = None
         self._grow(max_batch)
@@ -277,6 +281,8 @@ class BevVoxelizer:
         offs_c = (ctypes.c_int64 * (B + 1))(*offs.tolist())
         if self.force_atomic:
             flags |= _lib.BEV_FORCE_ATOMIC
+        if self.strip8:
+            flags |= _lib.BEV_STRIP8
         check(lib().sfa_bev_voxelize(points.data_ptr() if points.numel() else None, offs_c, B,
                                      _boundary_arr(boundary), flags, layout, out.data_ptr(),
                                      self.scratch.data_ptr(),

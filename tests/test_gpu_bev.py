@@ -119,8 +119,9 @@ def test_cpu_input_refused():
 
 @pytest.mark.parametrize("flip", [False, True])
 def test_binned_path_equals_atomic_path(gpu, flip):
-    """The default blocked voxeliser (one pass bins each 1024 points by 8-row strips into its own
-    record region + table, each strip reduced in LDS) and round 2's binned one (count / scan /
+    """The default blocked voxeliser (one pass bins each 1024 points by 4-row strips into its own
+    record region + table, each strip reduced in LDS), the same with 8-row strips
+    (SFA_BEV_STRIP8) and round 2's binned one (count / scan /
     bin / strip, SFA_BEV_FORCE_BINNED) give the bits of the global-atomic one (flag SFA_BEV_FORCE_ATOMIC) in every layout, flipped or not,
     on a ragged batch with a saturated-density cell and an empty frame; both leave the scratch
     zeroed."""
@@ -140,11 +141,14 @@ def test_binned_path_equals_atomic_path(gpu, flip):
     for layout in (_lib.BEV_NCHW3_F64, _lib.BEV_NCHW3_F32, _lib.BEV_NHWC4_F32):
         blocked = vox(pts, offs, gc.BOUNDARY, layout=layout, flags=flags).cpu().numpy()
         assert _scratch_clean(vox)
+        strip8 = vox(pts, offs, gc.BOUNDARY, layout=layout, flags=flags | _lib.BEV_STRIP8).cpu().numpy()
+        assert _scratch_clean(vox)
         binned = vox(pts, offs, gc.BOUNDARY, layout=layout, flags=flags | _lib.BEV_FORCE_BINNED).cpu().numpy()
         assert _scratch_clean(vox)
         atomic = vox(pts, offs, gc.BOUNDARY, layout=layout, flags=flags | _lib.BEV_FORCE_ATOMIC).cpu().numpy()
         assert _scratch_clean(vox)
         np.testing.assert_array_equal(blocked, atomic)
+        np.testing.assert_array_equal(strip8, atomic)
         np.testing.assert_array_equal(binned, atomic)
     f64 = vox(pts, offs, gc.BOUNDARY, layout=_lib.BEV_NCHW3_F64).cpu().numpy()
     for i, c in enumerate(clouds):
