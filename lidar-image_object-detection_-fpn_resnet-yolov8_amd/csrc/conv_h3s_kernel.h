@@ -37,7 +37,8 @@ namespace sfa {
 // MFMAs of column blocks 1, 2, .. (W first, then the strip: the counted waits are unchanged)
 // instead of in a burst right after the barrier.
 // 4096 = no W DMA inside the K loop (the first k-step's W is reused; ablation of the W staging
-// latency, results wrong).
+// latency, results wrong), 8192 = the W DMA issued as usual but never waited for (its latency
+// hidden, its issue and traffic kept; ablation, results wrong).
 template <int BM, int BN, int WM, int EPI, int OCC, int ABL = 0>
 __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const ConvArgs a) {
   constexpr int NW = BM / WM, NT = NW * 64;
@@ -314,6 +315,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
   load_strip(s0, smem);
   load_w(wk0(s0, 0), WB);
   w_in_loop = true;
+  constexpr int WOUT = (ABL & 8192) != 0 ? NB - (NB_REM != 0 ? 1 : 0) : 0;  // ablation: W DMAs left in flight
   for (int sl = 0; sl < nsl; ++sl) {
     const int s = s0 + sl;
     const bool last = sl + 1 == nsl;
@@ -329,11 +331,11 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
             else
               asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           } else if (NS_REM == 0 || wave < NS_REM)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS + WOUT) : "memory");
           else
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS - 1) : "memory");
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS - 1 + WOUT) : "memory");
         } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WOUT) : "memory");
         }
         __builtin_amdgcn_s_barrier();
         const int wnext = kw < 2 ? wk0(s, kw + 1) : (last ? wk0(s, 2) : wk0(s + 1, 0));
@@ -356,11 +358,11 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
       }
       if (kw == 1) {
         if (NS_REM == 0 || wave < NS_REM)
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS + WOUT) : "memory");
         else
-          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS - 1) : "memory");
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS - 1 + WOUT) : "memory");
       } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WOUT) : "memory");
       }
       __builtin_amdgcn_s_barrier();  // W(t) (and the strip) landed for every wave; W(t-1) no longer read
       const int wnext = kw < 2 ? wk0(s, kw + 1) : (last ? wk0(s, 2) : wk0(s + 1, 0));

@@ -271,19 +271,17 @@ int main(int argc, char** argv) {
   // round 2: conv_r3_kernel (A in registers) against the round-1 defaults (first entry of each)
   // round 3: strip-kernel ablations / variants on the body shapes (4096 = no W DMA in the K loop,
   // 32 = no epilogue; 14 = pre-split 128-wide, 26 = spread DMA)
+  // 4096 = no W DMA in the K loop, 8192 = W DMA issued but never waited for (ablations)
   std::vector<Cand> n64 = {
-      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDR(128, 64, 32, EPI_STD, 4, 2, 555264, 1),
-      CANDR(128, 64, 32, EPI_STD, 3, 3, 547072, 1), CANDR(128, 64, 32, EPI_STD, 2, 3, 547072, 1),
+      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDTA(128, 64, 32, EPI_STD, 3, 4238),
+      CANDTA(128, 64, 32, EPI_STD, 3, 8334),
   };
   std::vector<Cand> stem = {
       CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
   };
-  // conv_r3 on the body shapes with a three-stage W ring: 547072 = R3_BODY + v_fma_mix split +
-  // scalar taps; 1603844 = + 3-block W read-ahead + half-tile stagger + s_setprio
   std::vector<Cand> nbig = {
-      CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDR(128, 128, 32, EPI_STD, 2, 2, 526592, 1),
-      CANDR(128, 128, 32, EPI_STD, 2, 3, 547072, 1), CANDR(128, 128, 32, EPI_STD, 2, 3, 1603844, 1),
-      CANDR(128, 128, 32, EPI_STD, 3, 3, 547072, 1), CANDR(256, 128, 32, EPI_STD, 1, 3, 1603844, 1),
+      CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDTA(128, 128, 32, EPI_STD, 2, 4106),
+      CANDTA(128, 128, 32, EPI_STD, 2, 8202),
   };
   std::vector<Cand> heads = {
       CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1),

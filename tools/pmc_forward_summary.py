@@ -49,8 +49,11 @@ for r0 in passes[0]:
     for kp in keyed_passes:
         row.update({k2: v for k2, v in kp[key].items() if k2 not in ("name", "grid", "dur_ns")})
     merged.append(row)
-# last forward: from the last nchw3_to_nhwc4 dispatch to the following kfpn_combine
+# last forward: from its first kernel (the layout pass until round 3, the stem since the stem reads
+# the input layout itself) to the following kfpn_combine
 starts = [i for i, r in enumerate(merged) if "nchw3_to_nhwc4" in r["name"]]
+if not starts:
+    starts = [i for i, r in enumerate(merged) if "stem_patch_pool" in r["name"]]
 s = starts[-1]
 e = next(i for i in range(s, len(merged)) if "kfpn_combine" in merged[i]["name"])
 fwd = merged[s:e + 1]
