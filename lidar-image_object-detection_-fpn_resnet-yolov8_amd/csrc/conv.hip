@@ -196,8 +196,14 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     else
       b.ksplit = pick_ksplit(a, a.Kpad / 32, r3_big);
     if (strip) {
+      // A/B (round 3): 256 x 128 strip tiles, one 8-wave block per CU (half the W DMA per output
+      // row; same per-element summation order, so the same bits) for the 256-wide (bit 2097152)
+      // / 128-wide (bit 8388608) unsplit strip convs
+      const bool s256 = b.ksplit == 1 && ((a.N == 256 && (a.tune & 2097152)) || (a.N == 128 && (a.tune & 8388608)));
       if (a.tune & 16)
         rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
+      else if (s256)
+        rc = launch_conv_h3s_cfg<256, 128, 32, EPI_STD, 1, H3S_128>(b, st);
       else if (a.tune & 2)
         rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3, 10>(b, st);
       if (!ok(rc)) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, H3S_128>(b, st);

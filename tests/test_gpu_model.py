@@ -328,6 +328,23 @@ def test_heads_grouped_bit_identical(golden, gpu, hw):
         np.testing.assert_array_equal(outs[2][h], outs[0][h], err_msg=h)
 
 
+@pytest.mark.parametrize("tune", [2097152, 8388608])
+def test_strip256_bit_identical(golden, gpu, tune):
+    """256 x 128 strip tiles (one 8-wave block per CU) for the 256- / 128-wide body convs: every
+    output element runs the same K loop (super-steps kh x chunk, then kw) as in the 128 x 128
+    tiles, so the bits equal the default's (608 x 608: the bench's geometry picks these tiles)."""
+    x = torch.from_numpy(synthetic.synthetic_bev(2, 608, 608, seed=53)).to(gpu)
+    outs = []
+    for t in (0, tune):
+        model = make_model(golden, gpu)
+        model._engine(gpu).set_option(_lib.OPT_CONV_TUNE, t)
+        model._engine(gpu).set_math(_math("fp16x3"))
+        with torch.no_grad():
+            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(outs[1][h], outs[0][h], err_msg=h)
+
+
 def test_head_probe_grouped(golden, gpu):
     """Probe with grouped heads: the one launch's duration in entry 0, zeros after it; results
     unchanged; per-level probing again once the option is off."""
