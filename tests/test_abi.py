@@ -174,7 +174,7 @@ def test_argument_errors_before_any_launch():
     offs = (ctypes.c_int64 * 2)(0, 10)
     bnd = (ctypes.c_double * 6)(0, 50, -25, 25, -2.73, 1.27)
     assert L.sfa_bev_voxelize(p, offs, 0, bnd, 0, 2, p, p, None) == -1
-    assert L.sfa_bev_voxelize(p, offs, 1, bnd, 16, 2, p, p, None) == -1  # unknown flag bit
+    assert L.sfa_bev_voxelize(p, offs, 1, bnd, 32, 2, p, p, None) == -1  # unknown flag bit
     assert L.sfa_bev_scratch_size(16) == 2 * 16 * 608 * 608 * 12  # atomic-path cells + binned records
     # kernel probe (bench roofline): null model / unknown flags / reading a disabled probe
     ms = (ctypes.c_float * 3)()
