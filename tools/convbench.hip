@@ -271,16 +271,17 @@ int main(int argc, char** argv) {
   // round 2: conv_r3_kernel (A in registers) against the round-1 defaults (first entry of each)
   // round 3: strip-kernel ablations / variants on the body shapes (4096 = no W DMA in the K loop,
   // 32 = no epilogue; 14 = pre-split 128-wide, 26 = spread DMA)
-  // 256-row strip tiles (8 waves, one block per CU): half the W DMA per output row
+  // existing strip-kernel epilogue / DMA options on the body shapes: 1024 = output staged in LDS and
+  // stored row-contiguous, 16 = spread DMA, 2048 = non-temporal stores
   std::vector<Cand> n64 = {
-      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDTA(256, 64, 32, EPI_STD, 1, 142),
+      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDTA(128, 64, 32, EPI_STD, 3, 1166),
+      CANDTA(128, 64, 32, EPI_STD, 3, 30), CANDTA(128, 64, 32, EPI_STD, 3, 1054),
   };
   std::vector<Cand> stem = {
       CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
   };
   std::vector<Cand> nbig = {
-      CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDTA(256, 128, 32, EPI_STD, 1, 10),
-      CANDTK(256, 128, 32, EPI_STD, 1, 10, 2),
+      CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDTA(128, 128, 32, EPI_STD, 2, 1034),
   };
   std::vector<Cand> heads = {
       CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1),
