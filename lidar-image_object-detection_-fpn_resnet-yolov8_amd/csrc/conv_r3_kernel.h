@@ -440,6 +440,13 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
 // stages. The delayed half reads the next tile's first W blocks ahead across its tile boundary
 // (that tile was published by the barrier before); the leading half reads them after its
 // barrier. Same products in the same order: bit-identical to the unstaggered loop.
+// 8388608 = (with the stagger, scalar taps and the chunk-major order; one segment, stride 1)
+// shifted A: the K-tile of tap (kh, kw + 1) holds, for output row m, the input pixel that tap
+// (kh, kw) held for row m + 1 (same image row), so for kw 1, 2 the lane takes its fragment from
+// its row-group neighbour by DPP (row_shl:1; lane 15 from the next sub-tile's lane 0 by
+// row_shr:15) instead of loading it, and only the lanes whose rule breaks load: row 15 of the
+// wave's last sub-tile (its neighbour is the next wave's row) and rows at the image's right edge
+// (the neighbour is the next image row). Same fragments: bit-identical.
 // The kernel body for output tile (and split-K slice) lbid; conv_r3_kernel maps blockIdx to lbid
 // with xcd_remap, conv_r3_group_kernel (grouped head launch) per level.
 template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int NSEG, int ABL = 0>
@@ -547,6 +554,15 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   };
 
   unsigned vmask[TM], abase[TM];
+  constexpr bool SHIFT_A = (ABL & 8388608) != 0 && FAST_A && CMAJ && STAG;
+  unsigned fixa = 0;  // SHIFT_A: bit mi = this lane's row of sub-tile mi loads its shifted fragment itself
+  if constexpr (SHIFT_A) {
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = m0 + wave * WM + mi * 16 + c16;
+      if ((m % a.OW) == a.OW - 1 || (mi == TM - 1 && c16 == 15)) fixa |= 1u << mi;
+    }
+  }
   if constexpr (FAST_A) {
     const ConvSeg& sg0 = a.seg[0];
 #pragma unroll
@@ -573,6 +589,35 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
       const unsigned off = ok ? abase[mi] + toff : 0x80000000u;
       raw[mi][0] = __builtin_amdgcn_raw_buffer_load_b128(rs0, off, 0, 0);
       raw[mi][1] = __builtin_amdgcn_raw_buffer_load_b128(rs0, off + 16u, 0, 0);
+    }
+  };
+  // SHIFT_A: the fragments of the next K-tile (tap kw > 0 of the same kh and chunk) from this
+  // tile's (still in raw: split at the top of the tile) by DPP, then the fix-up lanes' loads
+  auto shift_a = [&](int k0) {
+    constexpr int SHL1 = 0x101, SHR15 = 0x11F;  // DPP row_shl:1, row_shr:15 (rows of 16 lanes)
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          int nx = (int)raw[mi][h][v];
+          if (mi + 1 < TM)  // lane 15 of each row: lane 0 of the next sub-tile
+            nx = __builtin_amdgcn_update_dpp((int)raw[mi + 1][h][v], (int)raw[mi + 1][h][v], SHR15, 0xf, 0xf, false);
+          raw[mi][h][v] = (unsigned)__builtin_amdgcn_update_dpp(nx, (int)raw[mi][h][v], SHL1, 0xf, 0xf, false);
+        }
+    const ConvSeg& sg0 = a.seg[0];
+    const int tap = k0 >> sg0.logC, c0 = k0 & (sg0.C - 1);
+    const int kh = (tap * sg0.kdiv_mul) >> sg0.kdiv_sh, kw = tap - kh * sg0.KW;
+    const unsigned toff = (unsigned)((((kh * sg0.W + kw) << sg0.logC) + c0) << 2);
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      if ((fixa >> mi) & 1u) {
+        const bool ok = tap < 32 && ((vmask[mi] >> tap) & 1u);
+        const unsigned off = ok ? abase[mi] + toff : 0x80000000u;
+        raw[mi][0] = __builtin_amdgcn_raw_buffer_load_b128(rs0, off, 0, 0);
+        raw[mi][1] = __builtin_amdgcn_raw_buffer_load_b128(rs0, off + 16u, 0, 0);
+      }
     }
   };
   auto load_a_seg = [&](auto sgc, const __amdgpu_buffer_rsrc_t rs, int kl) {
@@ -738,7 +783,19 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
       }
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
-        if (ni == 0 && more_a && !(ABL & 131072)) load_a(kt0 + kt + 1);
+        if (ni == 0 && more_a && !(ABL & 131072)) {
+          if constexpr (SHIFT_A) {
+            const int kn = kt0 + kt + 1;
+            const int chunk = (kn * 7282) >> 16;
+            const int tap = kn - 9 * chunk;  // chunk-major: tap kn % 9 of chunk kn / 9
+            if (tap % 3 != 0)
+              shift_a(kcol(kn));
+            else
+              load_a(kn);
+          } else {
+            load_a(kt0 + kt + 1);
+          }
+        }
         {
           const bool late = HB && ni >= H2;                   // block in interval kt + 1
           const int r = HB ? (late ? ni - H2 : ni + H2) : ni;  // compile-time for each HB
@@ -975,6 +1032,10 @@ inline int conv_r3_check(const ConvArgs& a) {
   }
   if ((ABL & 16384) != 0 && (a.nseg != 1 || a.seg[0].C < 32 || a.seg[0].taps > 32)) {
     set_error("conv_r3: fast A addressing needs one segment with C >= 32 (C=%d)", a.seg[0].C);
+    return SFA_E_UNSUPPORTED;
+  }
+  if ((ABL & 8388608) != 0 && (a.nseg != 1 || a.seg[0].stride != 1 || a.seg[0].KW != 3 || a.OW != a.seg[0].W)) {
+    set_error("conv_r3: shifted A needs one stride-1 3x3 segment (stride=%d KW=%d)", a.seg[0].stride, a.seg[0].KW);
     return SFA_E_UNSUPPORTED;
   }
   if ((ABL & 524288) != 0 && (a.seg[0].taps != 9 || a.seg[0].C % 32 != 0 ||

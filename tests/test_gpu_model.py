@@ -291,12 +291,13 @@ def test_round2_kernels_match_round1(golden, gpu, hw):
 @pytest.mark.parametrize("hw", [(160, 192), (96, 96), (608, 608)])
 def test_heads_stagger_bit_identical(golden, gpu, hw):
     """The heads conv with waves 4-7 half a K-tile behind their SIMD partners (three W stages, the
-    default; OPT_CONV_TUNE bit 131072 without the second half's s_setprio) adds the same products
-    in the same order as the unstaggered kernel (bit 65536): bit-identical outputs. Odd sizes
+    default; OPT_CONV_TUNE bit 131072 without the second half's s_setprio; bit 16777216 with the
+    taps kw 1, 2 shifted by DPP from the previous tap's fragments) adds the same products in the
+    same order as the unstaggered kernel (bit 65536): bit-identical outputs. Odd sizes
     cover partial tiles; K-tile counts 18 / 36 / 72 (C = 64 / 128 / 256) both parities."""
     x = torch.from_numpy(synthetic.synthetic_bev(2, hw[0], hw[1], seed=37)).to(gpu)
     outs = []
-    for flag in (0, 65536, 131072):
+    for flag in (0, 65536, 131072, 16777216):
         model = make_model(golden, gpu)
         model._engine(gpu).set_option(_lib.OPT_CONV_TUNE, flag)
         model._engine(gpu).set_math(_math("fp16x3"))
@@ -305,6 +306,7 @@ def test_heads_stagger_bit_identical(golden, gpu, hw):
     for h in gc.HEADS:
         np.testing.assert_array_equal(outs[1][h], outs[0][h], err_msg=h)
         np.testing.assert_array_equal(outs[2][h], outs[0][h], err_msg=h)
+        np.testing.assert_array_equal(outs[3][h], outs[0][h], err_msg=f"{h}: shifted A (tune 16777216)")
 
 
 @pytest.mark.parametrize("hw", [(160, 192), (96, 96), (608, 608)])

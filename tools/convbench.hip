@@ -283,8 +283,10 @@ int main(int argc, char** argv) {
   std::vector<Cand> nbig = {
       CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDTA(128, 128, 32, EPI_STD, 2, 1034),
   };
+  // heads: default stagger kernel vs shifted A (8388608: taps kw 1, 2 by DPP from the previous tap)
   std::vector<Cand> heads = {
-      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 3, 10057988, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 3, 10057988, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
