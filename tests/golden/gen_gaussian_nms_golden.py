@@ -10,6 +10,12 @@ are objects with ``.box`` ([x, y, w, h] ints, as the fusion scripts' boxes) and 
 and its ``calculate_iou(det, other_det)`` is test6.py:76-101 calculate_iou (also extracted with
 ``ast``) applied to the two boxes.  Inputs are seeded; inputs and outputs go to
 tests/golden/gaussian_nms_golden.npz.
+
+Why the reference's text is executed rather than oracle/fusion_oracle.gaussian_nms (advisor note,
+round 2): the fixtures pin the oracle; generated from the oracle they would pin nothing.  Only the
+two named FunctionDef nodes are compiled (no module-level statement of the README block or of
+test6.py runs), in a namespace holding numpy alone, in the build container, by hand — never by a
+test, smoke() or bench.py.
 """
 
 from __future__ import annotations
