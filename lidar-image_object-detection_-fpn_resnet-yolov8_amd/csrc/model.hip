@@ -300,6 +300,9 @@ struct sfa_model {
   hipStream_t side2 = nullptr;
   hipEvent_t join2 = nullptr;
   bool fpn3_side = false;  // (created only when enabled: every stream takes a hardware queue)
+  // A/B (env SFA_SIDE_PRIO, read at create): the side streams' priority, > 0 the device's lowest,
+  // < 0 its highest, 0 the default (hipStreamCreateWithFlags)
+  int side_prio = 0;
   int device = -1;
   std::mutex fork_mu;  // fork ... join of one forward is not interleaved with another's
   // Kernel probe (sfa_model_set_probe): timing events around each head-level launch, recorded
@@ -346,13 +349,20 @@ static void drop_side_streams(sfa_model* m) {
     }
 }
 
+static hipError_t side_stream_create(const sfa_model* m, hipStream_t* s) {
+  if (m->side_prio == 0) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  int least = 0, greatest = 0;
+  const hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e != hipSuccess) return e;
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, m->side_prio > 0 ? least : greatest);
+}
+
 static void make_side_streams(sfa_model* m) {
-  if (hipGetDevice(&m->device) != hipSuccess ||
-      hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking) != hipSuccess ||
+  if (hipGetDevice(&m->device) != hipSuccess || side_stream_create(m, &m->side) != hipSuccess ||
       hipEventCreateWithFlags(&m->fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&m->join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&m->mid, hipEventDisableTiming) != hipSuccess ||
-      (m->fpn3_side && (hipStreamCreateWithFlags(&m->side2, hipStreamNonBlocking) != hipSuccess ||
+      (m->fpn3_side && (side_stream_create(m, &m->side2) != hipSuccess ||
                         hipEventCreateWithFlags(&m->join2, hipEventDisableTiming) != hipSuccess))) {
     (void)hipGetLastError();
     drop_side_streams(m);
@@ -506,6 +516,7 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   if (const char* e = getenv("SFA_STEM_PATCH_ATOMIC")) m->stem_atomic = strcmp(e, "0") != 0;
   if (const char* e = getenv("SFA_FPN_COMMUTE")) m->fpn_commute = atoi(e) & 7;
   if (const char* e = getenv("SFA_FPN3_SIDE")) m->fpn3_side = strcmp(e, "0") != 0;
+  if (const char* e = getenv("SFA_SIDE_PRIO")) m->side_prio = atoi(e);
   if (const char* e = getenv("SFA_HEADS_GROUPED")) m->heads_grouped = std::min(std::max(atoi(e), 0), 2);
   bool side_streams = true;  // env SFA_SIDE_STREAMS=0: every launch on the caller's stream (A/B)
   if (const char* e = getenv("SFA_SIDE_STREAMS")) side_streams = strcmp(e, "0") != 0;
