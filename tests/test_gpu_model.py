@@ -437,6 +437,25 @@ def test_side_streams_off_on_bit_exact(golden, gpu):
         np.testing.assert_array_equal(base[h], on[h], err_msg=f"{h}: forward after re-creating them differs")
 
 
+@pytest.mark.parametrize("prio", ["1", "-1"])
+def test_side_stream_priority_bit_exact(golden, gpu, monkeypatch, prio):
+    """SFA_SIDE_PRIO (read when the model is created: its side streams at the device's lowest /
+    highest priority; an A/B knob) changes only scheduling: the same bits as the default."""
+    x = torch.from_numpy(synthetic.synthetic_bev(3, 160, 192, seed=59)).to(gpu)
+    outs = []
+    for env in (None, prio):
+        if env is None:
+            monkeypatch.delenv("SFA_SIDE_PRIO", raising=False)
+        else:
+            monkeypatch.setenv("SFA_SIDE_PRIO", env)
+        model = make_model(golden, gpu)
+        model._engine(gpu).set_math(_math("fp16x3"))
+        with torch.no_grad():
+            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(outs[1][h], outs[0][h], err_msg=h)
+
+
 @pytest.mark.parametrize("hw", [(160, 192), (608, 608)])
 def test_stem_input_layouts_bit_exact(golden, gpu, hw):
     """The patch stem reads the caller's layout itself (no conversion pass): NCHW3 (the
