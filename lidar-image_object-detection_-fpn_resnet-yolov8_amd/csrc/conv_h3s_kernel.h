@@ -38,7 +38,9 @@ namespace sfa {
 // instead of in a burst right after the barrier.
 // 4096 = no W DMA inside the K loop (the first k-step's W is reused; ablation of the W staging
 // latency, results wrong), 8192 = the W DMA issued as usual but never waited for (its latency
-// hidden, its issue and traffic kept; ablation, results wrong).
+// hidden, its issue and traffic kept; ablation, results wrong),
+// 16384 = A prefetch: the fragments of tap kw + 1 (same strip) are read and split during tap kw's
+// MFMAs (after column block TN / 2), so a k-step's first MFMAs wait only for their W fragments.
 template <int BM, int BN, int WM, int EPI, int OCC, int ABL = 0>
 __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const ConvArgs a) {
   constexpr int NW = BM / WM, NT = NW * 64;
@@ -228,8 +230,9 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     if (lane < 8) *reinterpret_cast<x6_f32x4*>(PH + (lane & 4 ? PR_BYTES : 0) + PROWS * 64 + (lane & 3) * 16) =
         x6_f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  auto compute = [&](const unsigned char* Ss, const unsigned char* Sw, int kw, auto&& issue) {
-    f16x8_t hf[2][TM];
+  constexpr bool APF = (ABL & 16384) != 0;
+  f16x8_t hfn[2][TM];  // APF: the next tap's split A fragments
+  auto read_a = [&](const unsigned char* Ss, int kw, f16x8_t (&hf)[2][TM]) {
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
       if constexpr (PS) {
@@ -261,6 +264,18 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
         hf[1][mi] = __builtin_shufflevector(t1, u1, 0, 1, 2, 3, 4, 5, 6, 7);
       }
     }
+  };
+  auto compute = [&](const unsigned char* Ss, const unsigned char* Sw, int kw, auto&& issue) {
+    f16x8_t hf[2][TM];
+    if (APF && kw > 0) {
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        hf[0][mi] = hfn[0][mi];
+        hf[1][mi] = hfn[1][mi];
+      }
+    } else {
+      read_a(Ss, kw, hf);
+    }
     const unsigned char* SB = Sw + c16 * BROW + ((gq ^ swzB(c16)) << 4);
     f16x8_t bq[3][2];
     auto read_b = [&](int ni) {
@@ -273,6 +288,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     for (int ni = 0; ni < TN; ++ni) {
       issue(ni);
       if (ni + 2 < TN) read_b(ni + 2);
+      if (APF && kw < 2 && ni == TN / 2) read_a(Ss, kw + 1, hfn);
       const f16x8_t c0 = bq[ni % 3][0], c1 = bq[ni % 3][1];
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {

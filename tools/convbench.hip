@@ -271,17 +271,17 @@ int main(int argc, char** argv) {
   // round 2: conv_r3_kernel (A in registers) against the round-1 defaults (first entry of each)
   // round 3: strip-kernel ablations / variants on the body shapes (4096 = no W DMA in the K loop,
   // 32 = no epilogue; 14 = pre-split 128-wide, 26 = spread DMA)
-  // existing strip-kernel epilogue / DMA options on the body shapes: 1024 = output staged in LDS and
-  // stored row-contiguous, 16 = spread DMA, 2048 = non-temporal stores
+  // 16384 = A prefetch: the next tap's fragments read and split during this tap's MFMAs
   std::vector<Cand> n64 = {
-      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDTA(128, 64, 32, EPI_STD, 3, 1166),
-      CANDTA(128, 64, 32, EPI_STD, 3, 30), CANDTA(128, 64, 32, EPI_STD, 3, 1054),
+      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDTA(128, 64, 32, EPI_STD, 3, 16526),
+      CANDTA(128, 64, 32, EPI_STD, 3, 142), CANDTA(128, 64, 32, EPI_STD, 3, 16526),
   };
   std::vector<Cand> stem = {
       CANDN(128, 64, 32, EPI_STD, 2, 16, 3, false, 0),
   };
   std::vector<Cand> nbig = {
-      CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDTA(128, 128, 32, EPI_STD, 2, 1034),
+      CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDTA(128, 128, 32, EPI_STD, 2, 16394),
+      CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDTA(128, 128, 32, EPI_STD, 2, 16394),
   };
   // heads: default stagger kernel vs shifted A (8388608: taps kw 1, 2 by DPP from the previous tap)
   std::vector<Cand> heads = {
