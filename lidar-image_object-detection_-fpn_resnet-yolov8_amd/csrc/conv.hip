@@ -154,6 +154,11 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
         rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD>(a, st);
       else if (a.tune & 131072)  // stagger without the second half's s_setprio (A/B)
         rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 3, R3_HEAD_STAG & ~4>(a, st);
+      else if ((a.tune & 33554432) && tile_rows(a) < 200000)
+        // round 3 (A/B): the level-0 heads (76 x 76) on 192 x 320 tiles of twelve 16-row waves, three
+        // per SIMD: 482 tiles fill 256 CUs 1.88 times instead of 361 tiles 1.41 times (same per-element
+        // K order: the same bits)
+        rc = launch_conv_r3_cfg<192, 320, 16, EPI_HEAD, 1, 3, R3_HEAD_STAG>(a, st);
       else if (a.tune & 16777216)  // round 3: shifted A fragments for taps kw 1, 2 (A/B)
         rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 3, R3_HEAD_STAG | 8388608>(a, st);
       else if (!(a.tune & 4))
@@ -316,7 +321,8 @@ int launch_conv_heads_group(const ConvArgs* lv, int n, int math, hipStream_t st)
   for (int i = 0; i < n; ++i) {
     if (!lv[i].wh || !lv[i].winv || lv[i].N != 320 || lv[i].tune != lv[0].tune) return SFA_E_UNSUPPORTED;
   }
-  if (lv[0].tune & (4 | 64 | 256 | 65536 | 131072 | 16777216)) return SFA_E_UNSUPPORTED;  // per-level A/B head kernels
+  if (lv[0].tune & (4 | 64 | 256 | 65536 | 131072 | 16777216 | 33554432))
+    return SFA_E_UNSUPPORTED;  // per-level A/B head kernels
   return launch_conv_r3_group_cfg<256, 320, 32, 1, 3, R3_HEAD_STAG>(lv, n, st);
 }
 

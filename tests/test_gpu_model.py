@@ -297,7 +297,7 @@ def test_heads_stagger_bit_identical(golden, gpu, hw):
     cover partial tiles; K-tile counts 18 / 36 / 72 (C = 64 / 128 / 256) both parities."""
     x = torch.from_numpy(synthetic.synthetic_bev(2, hw[0], hw[1], seed=37)).to(gpu)
     outs = []
-    for flag in (0, 65536, 131072, 16777216):
+    for flag in (0, 65536, 131072, 16777216, 33554432):
         model = make_model(golden, gpu)
         model._engine(gpu).set_option(_lib.OPT_CONV_TUNE, flag)
         model._engine(gpu).set_math(_math("fp16x3"))
@@ -307,6 +307,7 @@ def test_heads_stagger_bit_identical(golden, gpu, hw):
         np.testing.assert_array_equal(outs[1][h], outs[0][h], err_msg=h)
         np.testing.assert_array_equal(outs[2][h], outs[0][h], err_msg=h)
         np.testing.assert_array_equal(outs[3][h], outs[0][h], err_msg=f"{h}: shifted A (tune 16777216)")
+        np.testing.assert_array_equal(outs[4][h], outs[0][h], err_msg=f"{h}: 192-row level-0 tiles (tune 33554432)")
 
 
 @pytest.mark.parametrize("hw", [(160, 192), (96, 96), (608, 608)])

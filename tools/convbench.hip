@@ -283,10 +283,11 @@ int main(int argc, char** argv) {
       CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDTA(128, 128, 32, EPI_STD, 2, 16394),
       CANDTA(128, 128, 32, EPI_STD, 2, 10), CANDTA(128, 128, 32, EPI_STD, 2, 16394),
   };
-  // heads: default stagger kernel vs shifted A (8388608: taps kw 1, 2 by DPP from the previous tap)
+  // heads: default (256 x 320, 8 waves of 32 rows) vs 192 x 320 with 12 waves of 16 rows (3 per SIMD,
+  // 3-block W read-ahead so the stagger's ring repeats per tile)
   std::vector<Cand> heads = {
-      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 3, 10057988, 1),
-      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1), CANDR(256, 320, 32, EPI_HEAD, 1, 3, 10057988, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1), CANDR(192, 320, 16, EPI_HEAD, 1, 3, 1669380, 1),
+      CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1), CANDR(192, 320, 16, EPI_HEAD, 1, 3, 1669380, 1),
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
