@@ -176,6 +176,26 @@ def test_forward_608_math_modes(golden, gpu, math):
         assert e <= TOL
 
 
+@pytest.mark.parametrize("seed", [101, 202])
+def test_forward_608_weight_seeds(gpu, seed):
+    """More weight draws at full size: synthetic He-uniform weights (SURVEY §8(c)(i) conditioning,
+    the bench's kind) from two other seeds and a synthetic BEV frame; the default fp16x3 forward
+    within the logit bar of the CPU oracle forward for every head."""
+    from oracle import model_oracle
+    from sfa_hip import _lib, runtime
+    heads = runtime.DEFAULT_HEADS
+    arch = _lib.make_arch(heads)
+    sd = synthetic.synthetic_state_dict(_lib.state_layout(arch), seed)
+    eng = runtime.KfpnEngine(arch, runtime.pack_state_dict(sd, arch), gpu)
+    x = synthetic.synthetic_bev(1, 608, 608, seed=seed + 1)
+    out = eng.forward(torch.from_numpy(x).to(gpu))
+    ref = model_oracle.forward(model_oracle.state_dict_torch(sd), torch.from_numpy(x), heads)
+    for h in heads:
+        e = _err(out[h].cpu().numpy(), ref[h].numpy())
+        print(f"seed {seed} 608 {h}: max rel err {e:.3g}")
+        assert e <= TOL, h
+
+
 def test_stem_pool_fusion_bit_exact(golden, gpu):
     """fp16x3 stem with the max-pool fused into its epilogue (tile-border cells combined by
     atomicMax) == stem conv + maxpool3s2_kernel, bit for bit over the whole forward."""
