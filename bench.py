@@ -11,7 +11,11 @@ detections over RCCL (frames are sharded: rank r owns its own 16 frames).
 the GPU as well).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+       N > 1: either launched per rank by torch.distributed.run (RANK / WORLD_SIZE set), or
+       self-launched: with WORLD_SIZE unset the process touches no GPU, starts N rank processes
+       of itself (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) and exits with
+       the first failing rank's status (launch_ranks; the reference's own multi-process entry
+       spawns its ranks too: train.py:58-67 mp.spawn).
 Prints ONE JSON line on rank 0.
 """
 
@@ -21,6 +25,9 @@ import argparse
 import json
 import os
 import platform
+import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -114,6 +121,10 @@ def parse(argv=None):
                          "the configuration the roofline probe measures (for rocprof agreement)")
     ap.add_argument("--probe-forwards", type=int, default=10,
                     help="un-captured forwards timed per head launch for the roofline")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: every rank joins a gloo group and runs --steps all-gathers of "
+                         "rank-coded (B, K, 10) detections through sfa_hip.dist (rank wiring, the "
+                         "gather and the single JSON line; tests/test_bench_launcher.py)")
     args = ap.parse_args(argv)
     if args.inflight is None:
         args.inflight = 3 if args.workload == "fusion" else 2
@@ -128,10 +139,150 @@ def side_streams_for(args, world, nf):
     return {"on": True, "off": False, "auto": world == 1 and nf <= 2}[args.side_streams]
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int, argv, poll_s: float = 0.05) -> int:
+    """--gpus N > 1 started without a launcher: start N rank processes of this script (same
+    argv) and wait for them.  Called before anything touches a GPU (no torch.cuda call, no HIP
+    library load), so every child initialises its own device from a fresh process.  Rank r gets
+    RANK = LOCAL_RANK = r, WORLD_SIZE = LOCAL_WORLD_SIZE = N, MASTER_ADDR = 127.0.0.1 and a free
+    MASTER_PORT (kept if the caller set one).  Rank 0's stdout is this process's (its JSON line
+    goes out unchanged; the other ranks print none).  The first rank to exit non-zero ends the
+    others (SIGTERM, then SIGKILL after 10 s) so no survivor waits on a collective forever, and
+    its status is returned; 0 when every rank exits 0.  The ranks stay in this process's
+    process group (a timeout that kills the group ends them too), a SIGTERM / SIGINT to this
+    process is passed on to them, and each rank gets SIGTERM if this process dies
+    (PR_SET_PDEATHSIG)."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+
+    def _pdeathsig():
+        try:
+            import ctypes
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, int(signal.SIGTERM))  # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+
+    procs = []
+
+    def _end(live, sig):
+        for q in live:
+            try:
+                q.send_signal(sig)
+            except ProcessLookupError:
+                pass
+
+    def _forward(signo, _frame):
+        _end([p for p in procs if p.poll() is None], signo)
+        raise SystemExit(128 + signo)
+
+    old = {s: signal.signal(s, _forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                       LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                          preexec_fn=_pdeathsig))
+        status = 0
+        live = list(procs)
+        while live:
+            for p in list(live):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                live.remove(p)
+                if rc != 0 and status == 0:
+                    status = rc if rc > 0 else 128 - rc  # killed by a signal: 128 + signo, as a shell reports
+                    _end(live, signal.SIGTERM)
+                    deadline = time.time() + 10
+                    for q in live:
+                        try:
+                            q.wait(timeout=max(0.1, deadline - time.time()))
+                        except subprocess.TimeoutExpired:
+                            q.kill()
+                            q.wait()
+                    live = []
+                    break
+            if live:
+                time.sleep(poll_s)
+        return status
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+
+
+def run_dry(args):
+    """--dry-run: the N > 1 wiring without a GPU.  Each rank joins a gloo group, enqueues
+    --warmup + --steps all-gathers of its (B, K, 10) detections whose values encode (rank, step)
+    through sfa_hip.dist.gather_detections (the bench's collective, CPU tensors), checks every
+    gathered row and id, and the max-over-ranks time gives the JSON line rank 0 prints.
+    SFA_BENCH_FAIL_RANK=r makes rank r exit 3 after joining the group (exit-status tests)."""
+    import torch.distributed as dist
+    from sfa_hip import dist as sdist
+    rank, world = int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    if os.environ.get("SFA_BENCH_FAIL_RANK", "") == str(rank):
+        sys.stderr.write(f"rank {rank}: SFA_BENCH_FAIL_RANK\n")
+        sys.stderr.flush()
+        os._exit(3)
+    B, K = args.batch, args.K
+
+    def step(k):
+        dets = torch.zeros((B, K, 10), dtype=torch.float32)
+        dets[:, :, 0] = float(rank)
+        dets[:, :, 1] = float(k)
+        ids = torch.arange((k * world + rank) * B, (k * world + rank + 1) * B, dtype=torch.int64)
+        if world == 1:
+            return dets, ids
+        d, i = sdist.gather_detections(dets, ids)
+        exp = torch.cat([torch.arange((k * world + r) * B, (k * world + r + 1) * B) for r in range(world)])
+        if not torch.equal(i, exp) or not torch.equal(d[:, :, 0], torch.arange(world).repeat_interleave(B)
+                                                        .float()[:, None].expand(-1, K)) \
+                or not bool(torch.all(d[:, :, 1] == float(k))):
+            raise SystemExit(f"rank {rank}: gathered detections / ids of step {k} are wrong")
+        return d, i
+
+    for k in range(args.warmup):
+        step(k)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(args.warmup + k)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        frames = world * B * args.steps
+        print(json.dumps({
+            "metric": METRIC, "value": round(frames / max(elapsed, 1e-9), 2), "unit": "frames/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / max(1, args.steps) * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "dry_run": True,
+            "config": {"workload": "dry run: gloo all-gather of rank-coded (B, K, 10) detections only "
+                                   "(no GPU, no model)", "global_batch": world * B,
+                       "parallelism": f"dp{world}", "launcher": os.environ.get("SFA_BENCH_LAUNCHER", "external")},
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def init_dist(n):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != n:
-        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {n} but WORLD_SIZE={world}: start the ranks with torch.distributed.run "
+                         "--nproc-per-node N, or run without WORLD_SIZE set and bench.py launches them")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # SFA_BENCH_SHARE_DEVICE=1 + SFA_DIST_BACKEND=gloo: rehearse the N>1 path on one GPU
@@ -682,6 +833,16 @@ def runtime_make_calib(c):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: this process only starts the ranks (it never touches a GPU)
+        os.environ["SFA_BENCH_LAUNCHER"] = "bench.py"
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.dry_run:
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        if world != args.gpus:
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+        run_dry(args)
+        return
     rank, world, dev = init_dist(args.gpus)
     if args.workload in ("stream", "fusion"):
         if args.workload == "fusion":
