@@ -458,8 +458,8 @@ def traffic_per_forward(args):
         return int(json.load(f)["conv_hbm_bytes_per_forward"])
 
 
-def head_traffic_per_launch(args, grouped=False):
-    """HBM bytes per head launch (mean over the 3 levels; grouped: the one launch) from the committed PMC pass
+def head_traffic_per_launch(args):
+    """HBM bytes per head launch (mean over the 3 levels) from the committed PMC pass
     (tools/pmc_forward.sh: FETCH_SIZE x2 + WRITE_SIZE per dispatch, the probe's serial forward)."""
     if args.workload != "bev_infer" or args.batch != 16 or args.math != "fp16x3":
         return None
@@ -469,9 +469,6 @@ def head_traffic_per_launch(args, grouped=False):
         return None
     with open(files[-1]) as f:
         per = json.load(f)["per_launch"]
-    if grouped:  # one launch for the three levels
-        rows = [r for r in per if r["kernel"].startswith("sfa::conv_r3_group_kernel<256, 320")]
-        return int(rows[0]["hbm_MB"] * 1e6) if len(rows) == 1 else None
     rows = [r for r in per if r["kernel"].startswith("sfa::conv_r3_kernel<256, 320")]
     return int(sum(r["hbm_MB"] for r in rows) * 1e6 / len(rows)) if len(rows) == 3 else None
 
@@ -542,11 +539,11 @@ def probe_bev(args, pipe, reps=20):
     return {"bound": "hbm", "unit": "GB/s", "achieved": round(ach, 1), "peak": 8000.0,
             "frac": round(ach / 8000.0, 4), "traffic": traffic,
             "traffic_basis": "PMC 2 x FETCH_SIZE + WRITE_SIZE of one call (profiles/r*_pmc_bev.json): points read "
-                             "once by the bin pass, 16-B records written and read once, the top points' intensities "
+                             "once by the bin pass, 8-B records written and read once, the top points' intensities "
                              "gathered, the NCHW3 f32 map written",
             "kernel": "sfa_bev_voxelize (SFA_BEV_RAW: filter fused; bev_blk_bin_kernel: 1024 points per block "
-                      "binned by 8-row strip into the block's record region; bev_blk_strip_kernel: each strip "
-                      "reduced in LDS)",
+                      "binned by 4-row strip into the block's record region of 8-B records; bev_blk_strip_kernel: "
+                      "each strip reduced in LDS)",
             "us_per_batch": round(1e3 * ms, 1), "points_per_batch": npts,
             "algorithmic_bytes_per_batch": algo,
             "measured": "HIP events around %d back-to-back voxelisations of the step's %d sweeps, "
@@ -567,28 +564,6 @@ def roofline_line(args, heads, forward_roofline, fwd_achieved, peak, peak_basis,
         return line
     flops = head_flop_per_launch(args)
     ach = sum(flops) / (sum(heads) * 1e-3) / 1e12
-    grouped = len(heads) == 3 and heads[0] > 0 and heads[1] == 0 and heads[2] == 0
-    if grouped:  # SFA_OPT_HEADS_GROUPED: the three levels in one launch (probe entry 0)
-        line.update({
-            "kernel": "conv_r3_group_kernel<256, 320, ...> (fused detection heads of all three KFPN levels "
-                      "in ONE launch: 3x3 conv C->5x64 + bias + ReLU + the 5 heads' 1x1 convs; level tiles "
-                      "ordered by K, longest first)",
-            "achieved": round(ach, 3), "frac": round(ach / peak, 4),
-            "frac_of_power_capped": round(ach / capped, 4) if capped else None,
-            "frac_of_f32_mfma_peak": round(ach / PEAK_FP32_MFMA_TFLOPS, 4),
-            "measured": "HIP events on the launching stream around the grouped head launch, median of %d "
-                        "un-captured forwards, one step in flight (sfa_model_set_probe); achieved = "
-                        "algorithmic FLOP of the three levels / the launch's duration" % args.probe_forwards,
-            "grouped": True,
-            "launch_us": [round(1e3 * heads[0], 1)],
-            "avg_launch_us": round(1e3 * heads[0], 1),
-            "per_level_equivalent_us": round(1e3 * heads[0] / 3, 1),
-            "algorithmic_flop_per_launch": [sum(flops)],
-            "traffic": head_traffic_per_launch(args, grouped=True),
-            "traffic_basis": "HBM bytes of the grouped launch: PMC 2 x FETCH_SIZE + WRITE_SIZE "
-                             "(tools/pmc_forward.sh, profiles/r*_pmc_forward_%s.json)" % args.math,
-        })
-        return line
     line.update({
         "kernel": {"fp16x3": "conv_r3_kernel<256, 320, ...> (fused detection heads: 3x3 conv C->5x64 + bias + "
                              "ReLU + the 5 heads' 1x1 convs; one launch per KFPN level)",

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define SFA_ABI_VERSION 1
+#define SFA_ABI_VERSION 2  /* 2: sfa_bev_voxelize takes scratch_bytes */
 
 enum sfa_status {
   SFA_OK = 0,
@@ -57,9 +57,11 @@ const char* sfa_last_error_string(void);
  *                 | SFA_BEV_FLIP_HW: the map is written flipped in both spatial
  *                 dims (torch.flip(bev, [1, 2]), utils/demo_utils.py:110-111 — the
  *                 back view of demo_2_sides.py with boundary_back)
- * scratch         device, sfa_bev_scratch_size(batch) bytes, ZERO on first use;
- *                 every call leaves it zeroed again (except the binned path's record
- *                 region, which is written before it is read).
+ * scratch         device, scratch_bytes >= sfa_bev_scratch_size(batch) bytes (else
+ *                 SFA_E_WORKSPACE), ZERO on first use; every call leaves it zeroed again
+ *                 except the record regions, which are written before they are read.  The
+ *                 layout is set by the capacity (the largest batch scratch_bytes holds), not
+ *                 by the call's batch, so calls of any batch may share one scratch.
  * Kernels: one pass bins every 1024 points of a frame by 4-row strips of the map into
  * the pass block's own record region + a per-strip table, then one block per (frame, strip)
  * reduces its runs in LDS, while the batch's regions fit the scratch (~277 k points per
@@ -77,7 +79,7 @@ enum sfa_bev_flags {
 size_t sfa_bev_scratch_size(int batch);
 int sfa_bev_voxelize(const float* points, const int64_t* frame_offsets, int batch,
                      const double* boundary, int flags, int out_layout, void* out, void* scratch,
-                     void* stream);
+                     size_t scratch_bytes, void* stream);
 
 /* Replaces data_process/kitti_data_utils.py:228-251 get_filtered_lidar (labels=None):
  * order-preserving compaction of the points inside the inclusive box, with
@@ -126,8 +128,7 @@ int sfa_pack_weights(const sfa_arch* arch, const float* state, size_t state_floa
  * must outlive the handle).  No device memory is allocated.  The handle owns side
  * streams + events on the device current at creation: a forward on a stream of that
  * device runs the level-0 detection heads on a side stream (overlapping the rest of the FPN)
- * and the level-2 heads beside the level-1 heads (env SFA_FPN3_SIDE=1: the last FPN conv
- * pair too, on a second side stream), forked/joined by events, so HIP-graph capture of the
+ * and the level-2 heads beside the level-1 heads, forked/joined by events, so HIP-graph capture of the
  * caller's stream records every branch; on another device everything stays on the caller's
  * stream. */
 typedef struct sfa_model sfa_model;
@@ -158,29 +159,19 @@ enum sfa_math { SFA_MATH_F32 = 0, SFA_MATH_BF16X6 = 1, SFA_MATH_FP16X3 = 2 };
 int sfa_model_set_math(sfa_model* model, int math);
 int sfa_model_get_math(const sfa_model* model);
 
-/* Kernel-choice options of a model handle (no reference counterpart: A/B runs and the
- * kernel-equivalence tests).  Every option is a field of the handle, read by the forward when
- * it enqueues its launches (a captured graph keeps the choice of its capture); nothing on the
- * launch path reads the environment.  Defaults are the production kernels; at sfa_model_create
- * the env variable named beside each key seeds it (A/B scripts), sfa_model_set_option
- * overrides it.  Not concurrently with a forward of this model.
- *   SFA_OPT_CONV_TUNE        (SFA_TUNE)             bit mask returning conv groups to earlier
- *                                                   kernels (csrc/conv.hip); 0 = defaults
- *   SFA_OPT_STEM_PATCH       (SFA_STEM_PATCH)       1: stem + pool from LDS input patches (default)
- *   SFA_OPT_STEM_POOL_FUSION (SFA_STEM_POOL_FUSION) 1: max-pool fused into the stem (default)
- *   SFA_OPT_STEM_PATCH_ATOMIC(SFA_STEM_PATCH_ATOMIC)1: patch stem's border cells by atomicMax
- *   SFA_OPT_FPN_COMMUTE      (SFA_FPN_COMMUTE)      bit mask of FPN levels run commuted (7)
- *   SFA_OPT_FPN3_SIDE        (SFA_FPN3_SIDE)        1: second side stream (re-creates streams)
- *   SFA_OPT_STEM_ABL         (SFA_STEM_ABL)         patch-stem timing ablations (wrong results)
- *   SFA_OPT_HEADS_GROUPED    (SFA_HEADS_GROUPED)    the three levels' heads as ONE launch after the
- *                                                   FPN (fp16x3; bit-identical): 1 always, 0 never
- *                                                   (default), 2 when the model has no side stream
+/* Kernel-choice options of a model handle (no reference counterpart: the equivalence tests and
+ * A/B runs of the two forms each option selects).  Every option is a field of the handle, read by
+ * the forward when it enqueues its launches (a captured graph keeps the choice of its capture);
+ * nothing on the launch path reads the environment.  Defaults are the production kernels; at
+ * sfa_model_create the env variable named beside each key seeds it, sfa_model_set_option
+ * overrides it.  Not concurrently with a forward of this model.  (Round 4: the round-2/3 tune
+ * bits, stem ablations, grouped heads and second side stream — measured and not adopted — moved to
+ * tools/experiments/r03 with their convbench hooks.)
+ *   SFA_OPT_STEM_PATCH  (SFA_STEM_PATCH)  1: fp16x3 stem + max-pool from LDS input patches in one
+ *                                         kernel (default); 0: the implicit-GEMM stem + max-pool
+ *   SFA_OPT_FPN_COMMUTE (SFA_FPN_COMMUTE) bit mask of the FPN levels run commuted (7, fp16x3)
  */
-enum sfa_model_option {
-  SFA_OPT_CONV_TUNE = 0, SFA_OPT_STEM_PATCH = 1, SFA_OPT_STEM_POOL_FUSION = 2,
-  SFA_OPT_STEM_PATCH_ATOMIC = 3, SFA_OPT_FPN_COMMUTE = 4, SFA_OPT_FPN3_SIDE = 5, SFA_OPT_STEM_ABL = 6,
-  SFA_OPT_HEADS_GROUPED = 7
-};
+enum sfa_model_option { SFA_OPT_STEM_PATCH = 0, SFA_OPT_FPN_COMMUTE = 1 };
 int sfa_model_set_option(sfa_model* model, int key, int value);
 int sfa_model_get_option(const sfa_model* model, int key, int* value);
 
@@ -190,8 +181,7 @@ int sfa_model_get_option(const sfa_model* model, int key, int* value);
  * that launches it; SFA_PROBE_SERIAL: all launches stay on the caller's stream (no
  * side streams), so each head launch has the chip to itself.  sfa_model_probe_times
  * waits for the last probed forward's events and returns the launch durations of head
- * levels 0 .. n-1 in ms (grouped heads, SFA_OPT_HEADS_GROUPED: the one launch's duration in
- * entry 0, zeros after it).  flags = 0 turns the probe off. */
+ * levels 0 .. n-1 in ms.  flags = 0 turns the probe off. */
 enum sfa_probe_flags { SFA_PROBE_HEADS = 1, SFA_PROBE_SERIAL = 2 };
 int sfa_model_set_probe(sfa_model* model, int flags);
 int sfa_model_probe_times(const sfa_model* model, float* ms, int n);

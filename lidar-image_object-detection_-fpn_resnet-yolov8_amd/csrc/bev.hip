@@ -517,12 +517,29 @@ extern "C" size_t sfa_bev_scratch_size(int batch) {
   return 2 * bev_atomic_bytes(batch);
 }
 
+// The scratch layout is fixed by the scratch's CAPACITY (the largest batch it was sized for), never
+// by the batch of the call: keys / counts (atomic path, zero between calls) and the binned path's
+// counters (zero between calls) sit at the same offsets for every call, and the record regions
+// (written before they are read, left dirty) always lie after them.  A layout by the call's batch
+// let a small-batch call's records land inside a later larger call's zero areas.
+static int bev_capacity_batch(size_t scratch_bytes) {
+  int cap = 0;
+  while (cap < SFA_BEV_MAX_BATCH && sfa_bev_scratch_size(cap + 1) <= scratch_bytes) ++cap;
+  return cap;
+}
+
 extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offsets, int batch,
                                 const double* boundary, int flags, int out_layout, void* out,
-                                void* scratch, void* stream) {
+                                void* scratch, size_t scratch_bytes, void* stream) {
   SFA_CHECK_ARG(batch >= 1 && batch <= SFA_BEV_MAX_BATCH, "bev: batch %d out of [1, %d]", batch,
                 SFA_BEV_MAX_BATCH);
   SFA_CHECK_ARG(frame_offsets && boundary && out && scratch, "bev: null argument");
+  const int cap = bev_capacity_batch(scratch_bytes);
+  if (cap < batch) {
+    set_error("bev: scratch of %zu bytes holds %d frames, batch is %d (sfa_bev_scratch_size)", scratch_bytes, cap,
+              batch);
+    return SFA_E_WORKSPACE;
+  }
   SFA_CHECK_ARG(out_layout >= 0 && out_layout <= 2, "bev: bad out_layout %d", out_layout);
   SFA_CHECK_ARG((flags & ~(SFA_BEV_PREFILTERED | SFA_BEV_FLIP_HW | SFA_BEV_FORCE_ATOMIC | SFA_BEV_FORCE_BINNED |
                            SFA_BEV_STRIP8)) == 0,
@@ -562,7 +579,7 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
   auto* keys = reinterpret_cast<unsigned long long*>(scratch);
   auto* counts = reinterpret_cast<unsigned*>(
       reinterpret_cast<char*>(scratch) +
-      align_up((size_t)batch * kBevCells * sizeof(unsigned long long), 256));
+      align_up((size_t)cap * kBevCells * sizeof(unsigned long long), 256));
   const float4* p4 = reinterpret_cast<const float4*>(points);
   // blocked-bin path (default) when the batch's regions and table fit the binned scratch
   {
@@ -580,12 +597,12 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
     const size_t rec_bytes = align_up((size_t)nblk_total * kBlkPts * sizeof(uint2), 256);
     const size_t tab_bytes = (size_t)nblk_total * nstrips * sizeof(unsigned);
     // after the binned path's (zero) counters, which it must not touch
-    const size_t cnt_bytes = 3 * align_up((size_t)batch * kStrips * sizeof(unsigned), 256);
+    const size_t cnt_bytes = 3 * align_up((size_t)cap * kStrips * sizeof(unsigned), 256);
     int max_regions = 0;
     for (int b = 0; b < batch; ++b) max_regions = std::max(max_regions, bk.blk0[b + 1] - bk.blk0[b]);
     if (!force_atomic && !(flags_in & SFA_BEV_FORCE_BINNED) && max_regions <= maxr &&
-        cnt_bytes + rec_bytes + tab_bytes <= bev_atomic_bytes(batch)) {
-      char* sb = reinterpret_cast<char*>(scratch) + bev_atomic_bytes(batch) + cnt_bytes;
+        cnt_bytes + rec_bytes + tab_bytes <= bev_atomic_bytes(cap)) {
+      char* sb = reinterpret_cast<char*>(scratch) + bev_atomic_bytes(cap) + cnt_bytes;
       bk.rec = reinterpret_cast<uint2*>(sb);
       bk.tab = reinterpret_cast<unsigned*>(sb + rec_bytes);
       if (max_n > 0) {
@@ -623,12 +640,12 @@ extern "C" int sfa_bev_voxelize(const float* points, const int64_t* frame_offset
     }
   }
   // binned path (round 2) when forced or when the blocked regions do not fit
-  const size_t bin_bytes = align_up((size_t)batch * kStrips * sizeof(unsigned), 256);
-  const size_t binned_bytes = bev_atomic_bytes(batch);  // the binned path's region
+  const size_t bin_bytes = align_up((size_t)cap * kStrips * sizeof(unsigned), 256);
+  const size_t binned_bytes = bev_atomic_bytes(cap);  // the binned path's region
   const int64_t total = frame_offsets[batch] - frame_offsets[0];
   if (!force_atomic && 3 * bin_bytes < binned_bytes &&
       (uint64_t)total <= (uint64_t)((binned_bytes - 3 * bin_bytes) / sizeof(uint4)) && total < (int64_t)0xffffffff) {
-    char* sb = reinterpret_cast<char*>(scratch) + bev_atomic_bytes(batch);
+    char* sb = reinterpret_cast<char*>(scratch) + bev_atomic_bytes(cap);
     BinScratch bs;
     bs.count = reinterpret_cast<unsigned*>(sb);
     bs.offset = reinterpret_cast<unsigned*>(sb + bin_bytes);

@@ -186,14 +186,11 @@ struct ConvArgs {
   // upsampled x2 (align_corners, source step res_sh / res_sw), or null. bias may be null.
   const float* res_up;
   float res_sh, res_sw;
-  // Host-side kernel choice, copied from the model handle at each launch (never read from the
-  // environment on the launch path): SFA_OPT_CONV_TUNE bits (0 = the defaults, conv.hip) and
-  // SFA_OPT_STEM_ABL (timing ablations of the patch stem; wrong results by design).
+  // Round-3 experiment knobs (tools/experiments/r03 kernels and their convbench hooks only): tune
+  // bits, stem ablations, in-kernel split-K tickets. The product kernels never read them and the
+  // model leaves them zero.
   int tune;
   int stem_abl;
-  // Split-K tickets (model workspace, zero between launches; 2 words per output tile): when set,
-  // split-K launches combine their slices in the kernel (the last slice to arrive adds the others'
-  // partials in slice order and runs the epilogue) instead of a separate reduce launch.
   unsigned* tile_cnt;
   // Patch stem input (stem_patch_kernel.h): STEM_IN_NHWC4 (the voxeliser's layout), STEM_IN_NCHW3
   // (the reference's (B, 3, H, W)), STEM_IN_NCHW3_FLIP (read as torch.flip(x, [2, 3])); every

@@ -1,5 +1,5 @@
-// Convolution dispatch: picks the kernel (f32 MFMA or bf16x6) and its tile
-// configuration per layer shape (conv_kernel.h, conv_x6_kernel.h).
+// Convolution dispatch: picks the kernel (fp16x3, bf16x6 or f32 MFMA) and its tile
+// configuration per layer shape (conv_*_kernel.h).
 #include <cstdlib>
 
 #include "conv_kernel.h"
@@ -40,45 +40,14 @@ static int launch_conv_x6(const ConvArgs& a, int epilogue, hipStream_t st) {
   return rc;
 }
 
-static int num_cus() {
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0, n = 0;
-    ncu = (hipGetDevice(&dev) == hipSuccess &&
-           hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0)
-              ? n
-              : 256;
-  }
-  return ncu;
-}
-
-// Split-K slices of a 128 x 128-tiled body conv (fp16x3, standard epilogue with bias).
-// Default (round 2's rule): 2 slices for the 512-wide convs, combined by splitk_reduce_kernel.
-// OPT_CONV_TUNE bit 1024 (experimental, measured slower: model.hip tuned()) combines the slices
-// in the kernel (a.tile_cnt: the last slice adds the others' partials) and balances the grid —
-// 2 blocks per CU run at once and a block's time is set by its K steps, so the count minimises
-// ceil(tiles * ks / slots) / ks (+ 5 % of a block per extra slice) over the divisors of the
-// conv's K steps; bits 12..15 force a count. Tiles are priced at 16 frames of the conv's
-// geometry, so a frame's arithmetic never depends on its batch.
-static int pick_ksplit(const ConvArgs& a, int ksteps, bool inkernel) {
+// Split-K slices of a 128 x 128-tiled body conv (fp16x3, standard epilogue with bias): 2 for the
+// 512-wide (layer4) convs, whose 184 output tiles cannot fill 256 CUs (-13..16 %), combined by
+// splitk_reduce_kernel. Chosen from the conv width only, so a frame's arithmetic never depends
+// on its batch. (Balanced split counts with the slices combined in the kernel were measured 35 %
+// slower: tools/experiments/r03, profiles/r03e_ab_splitk_inkernel.txt.)
+static int pick_ksplit(const ConvArgs& a) {
   if (!a.part || !a.bias || a.wstride || a.wk0 || a.res_up) return 1;
-  const int forced = (a.tune >> 12) & 15;
-  if (forced) return ksteps % forced == 0 ? forced : 1;
-  if (!(a.tune & 1024) || !inkernel || !a.tile_cnt) return a.N >= 512 ? 2 : 1;
-  const long long tiles = (tile_rows(a) + 127) / 128 * (a.N / 128);
-  const long long slots = 2LL * num_cus();
-  int best = 1;
-  double best_cost = 1e30;
-  for (int ks = 1; ks <= 8; ++ks) {
-    if (ksteps % ks) continue;
-    const double rounds = (double)((tiles * ks + slots - 1) / slots);
-    const double cost = rounds / ks + 0.05 * (ks - 1);
-    if (cost < best_cost - 1e-9) {
-      best_cost = cost;
-      best = ks;
-    }
-  }
-  return best;
+  return a.N >= 512 ? 2 : 1;
 }
 
 // One-segment 3x3 / stride 1 / pad 1 conv with 32-channel chunks: conv_h3s_kernel applies.
@@ -88,55 +57,36 @@ static bool strip_ok(const ConvArgs& a) {
          (g.C & 31) == 0 && a.Kpad == 9 * g.C && a.OH == g.H && a.OW == g.W;
 }
 
-// fp16x3 tiles per shape (tools/convbench.hip sweeps: profiles/r01_convbench_h3n*.txt,
-// r01_convbench_h3m.txt, r01_convbench_strip_splitk.txt):
-//  * heads: conv_h3_kernel on 16x16x32 MFMAs, 256x320 (all 5 heads of a level per tile);
+// fp16x3 kernels per shape (tools/convbench.hip sweeps). Round 4 keeps only
+// the adopted kernels here; every measured-and-rejected variant (the round-2/3 SFA_TUNE bits) is in
+// tools/experiments/r03/ with its convbench hook.
+//  * heads: conv_r3_kernel 256 x 320 (all 5 heads of a level per tile), half-tile stagger, 3-stage
+//    W ring, 3-block W read-ahead, scalar taps, chunk-major K order, packed head epilogue;
 //  * 3x3/s1 body convs: conv_h3s_kernel (A staged once per kh as a row strip for the three kw
-//    taps): -4..5 % vs per-tap staging; 64-wide: 128x64 at 3 blocks/CU, 128..512-wide: 128x128.
-//    In isolation 64x128 tiles with 16-row wave tiles at 3 blocks/CU are 7-8 % faster on
-//    layer2/3 (profiles/r01_convbench_strip_tiles.txt) and the single-flight forward gains
-//    ~60 us, but with two steps in flight the bench loses ~1 % (profiles/r01_ab_strip_tiles.txt):
-//    kept selectable (SFA_TUNE bit 2), not the default;
-//  * the rest (stride-2 convs, 2-segment convs, 1x1 FPN convs, the stem): conv_h3_kernel,
-//    16x16x32 for the 64-wide ones, 32x32x16 for the 128..512-wide ones, BK 16 for the stem;
-//  * round 2: conv_r3_kernel (conv_r3_kernel.h: A fragments loaded straight into registers,
-//    only W through LDS, W DMA spread over the column blocks, transposed accumulators) for the
-//    heads and the big-M (layer2) convs the strip kernel cannot take (stride 2, conv +
-//    downsample segments); on layer3/4 shapes it does not beat the strip / conv_h3 kernels. The
-//    strip kernel runs in the transposed-accumulator form too (float4 epilogue: -7..11 %;
-//    profiles/r02_convbench_*.txt). SFA_TUNE bits 4 / 8 / 16 return the heads / the big-M
-//    non-strip convs / the strip convs to the round-1 kernels for same-box A/B, bit 32 the FPN
-//    skip convs, bit 64 the heads to the unpacked epilogue, bit 128 the 64-wide strip convs to
-//    no residual prefetch, bit 256 the conv_r3 launches to the tap-major K order, bit 512 the
-//    128..512-wide conv_h3 launches to the 32x32x16 MFMA form; round 3: bit 65536 the heads to
-//    the unstaggered kernel, bit 131072 to the stagger without s_setprio;
-//  * split-K 2 for the 512-wide (layer4) convs, whose 184 tiles cannot fill 256 CUs (-13..16 %);
-//    picked from the width only, so a frame's arithmetic never depends on the batch.
-// conv_x6g_kernel<..., PREC 1> tiles as the fallback.
-// Tuning knob for same-box A/B runs and the kernel-equivalence tests: ConvArgs::tune, set from
-// the model handle (sfa_model_set_option(SFA_OPT_CONV_TUNE); env SFA_TUNE seeds it when the
-// model is created), 0 = the defaults below. A captured graph keeps the kernels chosen at
-// capture time.
-
-// conv_r3_kernel variants (conv_r3_kernel.h ABL bits): W DMA spread over the column blocks (256),
-// transposed accumulators with float4 / permlane-swap epilogues (2048); heads also s_setprio 1
-// for the second half of the waves (4).
-// 524288: channel-chunk-major K order (the 3x3 window's 32-channel slices stay in L2 across the 9
-// taps; heads' HBM traffic 3.5-4.7x lower, -3..7 % per launch: profiles/r02_convbench_cmaj.txt)
+//    taps), transposed float4 epilogue, v_fma_mix split; 64-wide 128 x 64 at 3 blocks / CU with the
+//    pre-split strip and the residual loaded during the last super-step, 128..512-wide 128 x 128
+//    (split-K 2 for the 512-wide);
+//  * big-M (layer2) stride-2 and conv + downsample convs: conv_r3_kernel 128 x 128 (A in registers,
+//    chunk-major K), -25 % on layer2.0.conv1 against conv_h3;
+//  * FPN skip convs (half-resolution residual added bilinearly upsampled in the epilogue):
+//    conv_r3_kernel, float4 taps;
+//  * the rest (layer3/4 stride-2 and conv + downsample, the FPN low-resolution 1x1 convs, the stem
+//    without the patch kernel): conv_h3_kernel on 16x16x32 MFMAs.
+// conv_r3_kernel ABL values (conv_r3_kernel.h bit list): 256 spread W DMA | 2048 transposed
+// accumulators, always; 524288 chunk-major K order (the 3x3 window's 32-channel slices stay in L2
+// across the 9 taps; heads' HBM traffic 3.5-4.7x lower: profiles/r02_convbench_cmaj.txt);
+// 32768 the upsampled-residual epilogue (FPN skip convs).
 constexpr int R3_BODY = 256 | 2048 | 524288;
-constexpr int R3_FPN = 256 | 2048 | 32768;  // + the upsampled-residual epilogue (FPN skip convs)
-// strip kernel (conv_h3s_kernel.h ABL bits): transposed epilogue (2), v_fma_mix split (8); the
-// 64-wide also pre-split strip (4) and the residual tile loaded during the last super-step (128).
-// Non-temporal output stores (strip 2048, r3 262144) are 1-6 % faster per launch in isolation but
-// 1.2 % slower end to end (the next conv then reads its input from HBM): not used.
+constexpr int R3_FPN = 256 | 2048 | 32768;
+// heads: + s_setprio 1 for waves 4-7 (4), v_fma_mix split (4096), 3-block W read-ahead (8192), scalar
+// tap decode (16384), packed epilogue (65536), waves 4-7 half a K-tile behind their SIMD partners
+// with three W stages (1048576: -4.6 / -3.1 / -1.0 % per launch on L1 / L2 / L0, bit-identical,
+// profiles/r03h_convbench_heads_stagger.txt)
+constexpr int R3_HEAD_STAG = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536 | 524288 | 1048576;
+// strip kernel (conv_h3s_kernel.h bits): transposed epilogue (2) and v_fma_mix split (8); the
+// 64-wide also the pre-split strip (4) and the residual tile loaded during the last super-step (128)
 constexpr int H3S_64 = 2 | 4 | 8 | 128;
 constexpr int H3S_128 = 2 | 8;
-constexpr int R3_HEAD = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536 | 524288;  // + v_fma_mix split, 3-block W
-                                                                                 // read-ahead, scalar tap decode,
-                                                                                 // packed epilogue, chunk-major K
-// + waves 4-7 half a K-tile behind their SIMD partners (three W stages): heads L1 / L2 / L0
-// -4.6 / -3.1 / -1.0 % per launch in isolation, bit-identical (profiles/r03h_convbench_heads_stagger.txt)
-constexpr int R3_HEAD_STAG = R3_HEAD | 1048576;
 
 static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;
@@ -145,51 +95,19 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   const bool sliced = a.wstride || a.wk0 || a.res_up;  // conv_h3_kernel reads these; the others do not
   const bool strip = strip_ok(a) && !sliced;
   if (epilogue == EPI_HEAD) {
-    if (a.N == 320) {
-      if (a.tune & 64)  // the unpacked head epilogue (A/B)
-        rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD & ~65536>(a, st);
-      else if (a.tune & 256)  // tap-major K order (A/B)
-        rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD & ~524288>(a, st);
-      else if (a.tune & 65536)  // round 2: no stagger, two W stages, 3-block read-ahead (A/B)
-        rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 2, R3_HEAD>(a, st);
-      else if (a.tune & 131072)  // stagger without the second half's s_setprio (A/B)
-        rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 3, R3_HEAD_STAG & ~4>(a, st);
-      else if ((a.tune & 33554432) && tile_rows(a) < 200000)
-        // round 3 (A/B): the level-0 heads (76 x 76) on 192 x 320 tiles of twelve 16-row waves, three
-        // per SIMD: 482 tiles fill 256 CUs 1.88 times instead of 361 tiles 1.41 times (same per-element
-        // K order: the same bits)
-        rc = launch_conv_r3_cfg<192, 320, 16, EPI_HEAD, 1, 3, R3_HEAD_STAG>(a, st);
-      else if (a.tune & 16777216)  // round 3: shifted A fragments for taps kw 1, 2 (A/B)
-        rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 3, R3_HEAD_STAG | 8388608>(a, st);
-      else if (!(a.tune & 4))
-        rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 3, R3_HEAD_STAG>(a, st);
-      if (!ok(rc)) rc = launch_conv_h3_cfg<256, 320, 32, EPI_HEAD, 1, 32, 2, false, 2, 1>(a, st);
-      if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 320, 32, EPI_HEAD, 1, 16, 3, 0, 320, 1>(a, st);
-    }
-    if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_HEAD, 1, 16, 3, 0, 64, 1>(a, st);
+    if (a.N == 320) rc = launch_conv_r3_cfg<256, 320, 32, EPI_HEAD, 1, 3, R3_HEAD_STAG>(a, st);
+    if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_HEAD, 1, 16, 3, 0, 64, 1>(a, st);  // other head counts
     return rc;
   }
-  if (a.res_up && !(a.tune & 32) && (a.tune & 1048576)) {  // A/B: the residual's taps before the K loop
-    if (a.N == 64)
-      rc = launch_conv_r3_cfg<128, 64, 32, EPI_STD, 3, 2, R3_FPN | 4194304>(a, st);
-    else if (a.N % 128 == 0)
-      rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_FPN | 4194304>(a, st);
-    if (ok(rc)) return rc;
-  }
-  if (a.res_up && !(a.tune & 32)) {  // FPN skip convs: transposed float4 epilogue, float4 taps
+  if (a.res_up) {  // FPN skip convs: transposed float4 epilogue, float4 taps
     if (a.N == 64)
       rc = launch_conv_r3_cfg<128, 64, 32, EPI_STD, 4, 2, R3_FPN>(a, st);
     else if (a.N % 128 == 0)
       rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_FPN>(a, st);
-    if (ok(rc)) return rc;
+    return rc;
   }
   if (a.N == 64) {
-    if (strip) {
-      if (a.tune & 16) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3>(a, st);
-      else if (a.tune & 1) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 2>(a, st);
-      else if (a.tune & 128) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, 14>(a, st);  // round-2 A/B
-      else rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, H3S_64>(a, st);
-    }
+    if (strip) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, H3S_64>(a, st);
     if (!ok(rc) && a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 64, 32, EPI_STD, 2, 16, 3, false, 0>(a, st);
     if (!ok(rc) && !sliced) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_STD, 1, 16, 3, 0, 64, 1>(a, st);
@@ -197,41 +115,14 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   }
   if (a.N % 128 == 0) {
     ConvArgs b = a;
-    const bool r3_big = !strip && tile_rows(a) >= 50000 && !(a.tune & 8);  // conv_r3 below: in-kernel split
-    if (strip)
-      b.ksplit = pick_ksplit(a, 3 * (a.seg[0].C >> 5), !(a.tune & 16) && !(a.tune & 2));
-    else
-      b.ksplit = pick_ksplit(a, a.Kpad / 32, r3_big);
-    if (strip) {
-      // A/B (round 3): 256 x 128 strip tiles, one 8-wave block per CU (half the W DMA per output
-      // row; same per-element summation order, so the same bits) for the 256-wide (bit 2097152)
-      // / 128-wide (bit 8388608) unsplit strip convs
-      const bool s256 = b.ksplit == 1 && ((a.N == 256 && (a.tune & 2097152)) || (a.N == 128 && (a.tune & 8388608)));
-      if (a.tune & 16)
-        rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
-      else if (s256)
-        rc = launch_conv_h3s_cfg<256, 128, 32, EPI_STD, 1, H3S_128>(b, st);
-      else if (a.tune & 2)
-        rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3, 10>(b, st);
-      if (!ok(rc)) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, H3S_128>(b, st);
-    } else if (tile_rows(a) >= 50000 && !(a.tune & 8)) {  // big-M stride-2 / two-segment: A from registers
-      if (a.tune & 256)  // tap-major K order (A/B)
-        rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY & ~524288>(b, st);
-      else
-        rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
-    }
+    b.ksplit = pick_ksplit(a);
+    if (strip && (3 * (a.seg[0].C >> 5)) % b.ksplit == 0)
+      rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, H3S_128>(b, st);
+    else if (!strip && tile_rows(a) >= 50000)  // big-M stride-2 / two-segment: A from registers
+      rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
     if (!ok(rc)) {
-      // 16x16x32 MFMA form (round 2): -6 % per launch on layer3.0.conv1, +1.2 % end to end
-      // (profiles/r02_ab_h3_mf1.txt); SFA_TUNE bit 512 returns to the 32x32x16 form
-      if (a.tune & 512)
-        rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
-      else
-        rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2, 1>(b, st);
-    }
-    if (!ok(rc) && b.ksplit > 1) {  // K not divisible into the slices: no split
-      b.ksplit = 1;
-      if (strip) rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2>(b, st);
-      if (!ok(rc)) rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2>(b, st);
+      if ((a.Kpad / 32) % b.ksplit != 0) b.ksplit = 1;  // K not divisible into the slices: no split
+      rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2, 1>(b, st);
     }
     if (!ok(rc) && !sliced) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2, 16, 3, 0, 128, 1>(b, st);
   }
@@ -274,14 +165,6 @@ int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t st) {
     }
     return launch_conv_h3(a, epilogue, st);
   }
-  if (epilogue == EPI_POOL) {  // fused stem + max-pool: fp16x3 only; the caller falls back
-    if (math != SFA_MATH_FP16X3 || !a.wh || !a.winv || a.nseg != 1 || a.N != 64 || !a.relu || a.res ||
-        a.ksplit > 1 || a.OH % 8 != 0 || a.OW % 16 != 0) {
-      set_error("conv: fused max-pool epilogue unsupported here (OH=%d OW=%d N=%d)", a.OH, a.OW, a.N);
-      return SFA_E_UNSUPPORTED;
-    }
-    return launch_conv_h3_cfg<128, 64, 32, EPI_POOL, 2, 16, 3, false, 0, 0>(a, st);  // the stem's tile
-  }
   if (math == SFA_MATH_FP16X3) {
     const int rc = launch_conv_h3(a, epilogue, st);
     if (rc != SFA_E_UNSUPPORTED) return rc;
@@ -311,19 +194,6 @@ int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t st) {
       return launch_conv_cfg<64, 64, 32, 32, 32, EPI_STD, 4>(a, st);
   }
   return launch_conv_cfg<64, 64, 32, 32, 16, EPI_STD, 4>(a, st);
-}
-
-// The three KFPN levels' heads in one launch (conv_r3_group_kernel: longest K first, so the
-// per-level launches' partial last rounds of tiles become one short tail). fp16x3 and the
-// default head kernel only; SFA_E_UNSUPPORTED otherwise (the caller launches per level).
-int launch_conv_heads_group(const ConvArgs* lv, int n, int math, hipStream_t st) {
-  if (math != SFA_MATH_FP16X3 || n != 3) return SFA_E_UNSUPPORTED;
-  for (int i = 0; i < n; ++i) {
-    if (!lv[i].wh || !lv[i].winv || lv[i].N != 320 || lv[i].tune != lv[0].tune) return SFA_E_UNSUPPORTED;
-  }
-  if (lv[0].tune & (4 | 64 | 256 | 65536 | 131072 | 16777216 | 33554432))
-    return SFA_E_UNSUPPORTED;  // per-level A/B head kernels
-  return launch_conv_r3_group_cfg<256, 320, 32, 1, 3, R3_HEAD_STAG>(lv, n, st);
 }
 
 int launch_stem_patch(const ConvArgs& a, hipStream_t st) { return launch_stem_patch_pool(a, st); }

@@ -283,26 +283,14 @@ struct sfa_model {
   Plan plan;
   int math;
   int fpn_commute = 7;  // fp16x3: bit f -> FPN conv f as up(W_a x) + W_b skip (env SFA_FPN_COMMUTE, mask)
-  bool pool_fusion = true;  // fp16x3 stem + max-pool in one kernel (env SFA_STEM_POOL_FUSION=0: off)
-  bool stem_patch = true;   // ... from LDS input patches (stem_patch_kernel.h; env SFA_STEM_PATCH=0: off)
-  // patch stem's tile-border pooled cells: owner tile + side buffer + merge pass (default), or
-  // (env SFA_STEM_PATCH_ATOMIC=1) atomicMax into the zeroed pooled buffer — same bits, A/B only
-  bool stem_atomic = false;
+  // fp16x3 stem + max-pool from LDS input patches in one kernel (stem_patch_kernel.h; env
+  // SFA_STEM_PATCH=0: the implicit-GEMM stem conv + the max-pool kernel, as the other math modes)
+  bool stem_patch = true;
   // Side stream for the level-0 heads (they only need up_level2, so they overlap the rest
   // of the FPN and the level-1/2 heads); created with the model on the current device,
   // used only when the forward's stream is on that device.
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr, mid = nullptr;
-  // Second side stream (env SFA_FPN3_SIDE=1): the last FPN conv pair (conv_up_level3, ->
-  // up_level4) and the level-2 heads there, beside the level-1 heads, which need only
-  // up_level3. Off by default: the single-step forward gains 1-2 %, but with two steps in
-  // flight (the bench) the extra concurrency costs 1.7 % (profiles/r02_ab_fpn3_side.txt).
-  hipStream_t side2 = nullptr;
-  hipEvent_t join2 = nullptr;
-  bool fpn3_side = false;  // (created only when enabled: every stream takes a hardware queue)
-  // A/B (env SFA_SIDE_PRIO, read at create): the side streams' priority, > 0 the device's lowest,
-  // < 0 its highest, 0 the default (hipStreamCreateWithFlags)
-  int side_prio = 0;
   int device = -1;
   std::mutex fork_mu;  // fork ... join of one forward is not interleaved with another's
   // Kernel probe (sfa_model_set_probe): timing events around each head-level launch, recorded
@@ -310,60 +298,27 @@ struct sfa_model {
   // keeps every launch on the caller's stream so each head launch has the chip to itself.
   int probe = 0;
   hipEvent_t probe_ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  bool probe_grouped = false;  // the last probed forward's heads ran as one grouped launch (events 0, 1)
-  // kernel-choice options (sfa_model_set_option): conv tune bits, patch-stem ablation
-  int tune = 0;
-  int stem_abl = 0;
-  // heads as ONE launch of the three levels after the FPN (conv_r3_group_kernel): 1 always,
-  // 0 (default) never: one launch per level, 2 when the model has no side stream. Serially the
-  // grouped launch takes 7 % off the three per-level launches (their partial last rounds of
-  // tiles become one short tail), but with two steps in flight the other step's kernels fill
-  // those tails anyway: headline -0.8 %, stream workload -1.6 %, fusion +-0
-  // (profiles/r03n_ab_heads_grouped.txt) — kept for single-stream, one-step-at-a-time callers
-  int heads_grouped = 0;
 };
-
-// A conv's arguments with the model's kernel-choice options (ConvArgs::tune / stem_abl).
-static inline ConvArgs tuned(ConvArgs a, const sfa_model* m) {
-  a.tune = m->tune;
-  a.stem_abl = m->stem_abl;
-  // in-kernel split-K combining only on request (OPT_CONV_TUNE bit 1024): measured 35 % slower
-  // per forward than the reduce launch (profiles/r03e_ab_splitk_inkernel.txt) — the agent-scope
-  // fences a slice needs to publish its partial to another XCD write back / invalidate the L2
-  if (!(m->tune & 1024)) a.tile_cnt = nullptr;
-  return a;
-}
 
 // The model's side stream(s) and their events, created on the current device; on failure
 // (no device) none, and the forward runs every launch on the caller's stream.
 static void drop_side_streams(sfa_model* m) {
-  for (hipEvent_t* e : {&m->fork, &m->join, &m->mid, &m->join2})
+  for (hipEvent_t* e : {&m->fork, &m->join, &m->mid})
     if (*e) {
       (void)hipEventDestroy(*e);
       *e = nullptr;
     }
-  for (hipStream_t* s : {&m->side2, &m->side})
-    if (*s) {
-      (void)hipStreamDestroy(*s);
-      *s = nullptr;
-    }
-}
-
-static hipError_t side_stream_create(const sfa_model* m, hipStream_t* s) {
-  if (m->side_prio == 0) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-  int least = 0, greatest = 0;
-  const hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-  if (e != hipSuccess) return e;
-  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, m->side_prio > 0 ? least : greatest);
+  if (m->side) {
+    (void)hipStreamDestroy(m->side);
+    m->side = nullptr;
+  }
 }
 
 static void make_side_streams(sfa_model* m) {
-  if (hipGetDevice(&m->device) != hipSuccess || side_stream_create(m, &m->side) != hipSuccess ||
+  if (hipGetDevice(&m->device) != hipSuccess || hipStreamCreateWithFlags(&m->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&m->fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&m->join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&m->mid, hipEventDisableTiming) != hipSuccess ||
-      (m->fpn3_side && (side_stream_create(m, &m->side2) != hipSuccess ||
-                        hipEventCreateWithFlags(&m->join2, hipEventDisableTiming) != hipSuccess))) {
+      hipEventCreateWithFlags(&m->mid, hipEventDisableTiming) != hipSuccess) {
     (void)hipGetLastError();
     drop_side_streams(m);
   }
@@ -509,15 +464,8 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   m->math = SFA_MATH_FP16X3;
   // A/B convenience: the environment seeds the options once, here (sfa_model_set_option
   // overrides them; nothing reads the environment on the launch path)
-  if (const char* e = getenv("SFA_TUNE")) m->tune = atoi(e);
-  if (const char* e = getenv("SFA_STEM_ABL")) m->stem_abl = atoi(e);
-  if (const char* e = getenv("SFA_STEM_POOL_FUSION")) m->pool_fusion = strcmp(e, "0") != 0;
   if (const char* e = getenv("SFA_STEM_PATCH")) m->stem_patch = strcmp(e, "0") != 0;
-  if (const char* e = getenv("SFA_STEM_PATCH_ATOMIC")) m->stem_atomic = strcmp(e, "0") != 0;
   if (const char* e = getenv("SFA_FPN_COMMUTE")) m->fpn_commute = atoi(e) & 7;
-  if (const char* e = getenv("SFA_FPN3_SIDE")) m->fpn3_side = strcmp(e, "0") != 0;
-  if (const char* e = getenv("SFA_SIDE_PRIO")) m->side_prio = atoi(e);
-  if (const char* e = getenv("SFA_HEADS_GROUPED")) m->heads_grouped = std::min(std::max(atoi(e), 0), 2);
   bool side_streams = true;  // env SFA_SIDE_STREAMS=0: every launch on the caller's stream (A/B)
   if (const char* e = getenv("SFA_SIDE_STREAMS")) side_streams = strcmp(e, "0") != 0;
   if (side_streams) make_side_streams(m);
@@ -540,7 +488,6 @@ extern "C" int sfa_model_set_side_streams(sfa_model* model, int on) {
     // the side streams' last forward must be done before they go (the caller's stream has
     // joined them, so nothing enqueued later depends on them)
     SFA_HIP_TRY(hipStreamSynchronize(model->side));
-    if (model->side2) SFA_HIP_TRY(hipStreamSynchronize(model->side2));
     drop_side_streams(model);
   } else if (on && !model->side) {
     make_side_streams(model);
@@ -553,29 +500,10 @@ extern "C" int sfa_model_set_option(sfa_model* model, int key, int value) {
   SFA_CHECK_ARG(model, "set_option: null model");
   std::lock_guard<std::mutex> lk(model->fork_mu);
   switch (key) {
-    case SFA_OPT_CONV_TUNE: model->tune = value; break;
     case SFA_OPT_STEM_PATCH: model->stem_patch = value != 0; break;
-    case SFA_OPT_STEM_POOL_FUSION: model->pool_fusion = value != 0; break;
-    case SFA_OPT_STEM_PATCH_ATOMIC: model->stem_atomic = value != 0; break;
     case SFA_OPT_FPN_COMMUTE:
       SFA_CHECK_ARG(value >= 0 && value <= 7, "set_option: FPN_COMMUTE mask %d not in 0..7", value);
       model->fpn_commute = value;
-      break;
-    case SFA_OPT_FPN3_SIDE:
-      if ((value != 0) != model->fpn3_side) {
-        model->fpn3_side = value != 0;
-        if (model->side) {  // re-create the side streams with / without the second one
-          SFA_HIP_TRY(hipStreamSynchronize(model->side));
-          if (model->side2) SFA_HIP_TRY(hipStreamSynchronize(model->side2));
-          drop_side_streams(model);
-          make_side_streams(model);
-        }
-      }
-      break;
-    case SFA_OPT_STEM_ABL: model->stem_abl = value; break;
-    case SFA_OPT_HEADS_GROUPED:
-      SFA_CHECK_ARG(value >= 0 && value <= 2, "set_option: HEADS_GROUPED %d not in 0..2", value);
-      model->heads_grouped = value;
       break;
     default: set_error("set_option: unknown key %d", key); return SFA_E_INVALID;
   }
@@ -585,14 +513,8 @@ extern "C" int sfa_model_set_option(sfa_model* model, int key, int value) {
 extern "C" int sfa_model_get_option(const sfa_model* model, int key, int* value) {
   SFA_CHECK_ARG(model && value, "get_option: null argument");
   switch (key) {
-    case SFA_OPT_CONV_TUNE: *value = model->tune; break;
     case SFA_OPT_STEM_PATCH: *value = model->stem_patch; break;
-    case SFA_OPT_STEM_POOL_FUSION: *value = model->pool_fusion; break;
-    case SFA_OPT_STEM_PATCH_ATOMIC: *value = model->stem_atomic; break;
     case SFA_OPT_FPN_COMMUTE: *value = model->fpn_commute; break;
-    case SFA_OPT_FPN3_SIDE: *value = model->fpn3_side; break;
-    case SFA_OPT_STEM_ABL: *value = model->stem_abl; break;
-    case SFA_OPT_HEADS_GROUPED: *value = model->heads_grouped; break;
     default: set_error("get_option: unknown key %d", key); return SFA_E_INVALID;
   }
   return SFA_OK;
@@ -622,10 +544,6 @@ extern "C" int sfa_model_probe_times(const sfa_model* model, float* ms, int n) {
   SFA_CHECK_ARG(model && ms && n >= 0 && n <= 3, "probe_times: bad arguments");
   SFA_CHECK_ARG(model->probe & SFA_PROBE_HEADS, "probe_times: probe not enabled");
   for (int f = 0; f < n; ++f) {
-    if (model->probe_grouped && f > 0) {  // one grouped launch: its duration is level 0's entry
-      ms[f] = 0.f;
-      continue;
-    }
     SFA_HIP_TRY(hipEventSynchronize(model->probe_ev[2 * f + 1]));
     SFA_HIP_TRY(hipEventElapsedTime(&ms[f], model->probe_ev[2 * f], model->probe_ev[2 * f + 1]));
   }
@@ -636,8 +554,7 @@ namespace sfa {
 
 // Activation buffers of one forward (NHWC f32), carved from the workspace.
 struct Bufs {
-  size_t xin, s0, p0, t[4], a[4], l[4], up1, c1, up2, c2, up3, up4, L0, L1, L2, amax, cnt, cnt_words, part,
-      part_floats, total;
+  size_t xin, s0, p0, t[4], a[4], l[4], up1, c1, up2, c2, up3, up4, L0, L1, L2, amax, part, part_floats, total;
 };
 
 // fp16x3 activation maxima (conv.h): per tensor a conv reads (named by its producer), B
@@ -677,15 +594,10 @@ static Bufs plan_bufs(const sfa_arch* arch, int B, int H, int W) {
   b.L0 = take((size_t)nch * B * P8);
   b.L1 = take((size_t)nch * B * P4);
   b.L2 = take((size_t)nch * B * P4);
-  // the activation maxima, then the split-K tile tickets (2 words per 128 x 128 output tile of
-  // the most-tiled split conv, layer2: B (H / 8) (W / 8) / 128 rows of tiles); zeroed together
-  // once per forward
-  b.cnt_words = 2 * ((size_t)B * (H / 32) * (W / 32) / 8 + 64);
-  b.amax = take((size_t)AM_COUNT * B * SFA_AMAX_WORDS + b.cnt_words);
-  b.cnt = b.amax + (size_t)AM_COUNT * B * SFA_AMAX_WORDS * 4;
-  // split-K partial sums (conv.hip pick_ksplit: up to 8 slices of layer4, 4 of layer3, 2 of layer2:
-  // 8 * B * (H / 32) * (W / 32) * 512 floats hold each of them)
-  b.part_floats = (size_t)8 * B * (H / 32) * (W / 32) * 512;
+  // the activation maxima (zeroed once per forward)
+  b.amax = take((size_t)AM_COUNT * B * SFA_AMAX_WORDS);
+  // split-K partial sums (conv.hip pick_ksplit: 2 slices of the 512-wide layer4 convs)
+  b.part_floats = (size_t)2 * B * (H / 32) * (W / 32) * 512;
   b.part = take(b.part_floats);
   b.total = cur;
   return b;
@@ -779,21 +691,20 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   };
   auto blk_slot = [](int li, int bi, int ci) { return AM_BLK + 4 * li + 2 * bi + ci; };
   if (h3)
-    SFA_HIP_TRY(hipMemsetAsync(ws + bf.amax, 0, ((size_t)AM_COUNT * B * SFA_AMAX_WORDS + bf.cnt_words) * 4, st));
+    SFA_HIP_TRY(hipMemsetAsync(ws + bf.amax, 0, (size_t)AM_COUNT * B * SFA_AMAX_WORDS * 4, st));
   auto io = [&](ConvArgs& a, int in0, int in1, int out) {
     a.amax_in[0] = in0 >= 0 ? AM(in0) : nullptr;
     a.amax_in[1] = in1 >= 0 ? AM(in1) : nullptr;
     a.amax_out = out >= 0 ? AM(out) : nullptr;
     a.part = F(bf.part);
     a.part_floats = bf.part_floats;
-    a.tile_cnt = h3 ? reinterpret_cast<unsigned*>(ws + bf.cnt) : nullptr;
   };
 
   const int H2 = H / 2, W2 = W / 2;
-  const bool pool_fused = h3 && m->pool_fusion && H2 % 8 == 0 && W2 % 16 == 0;
-  // The patch stem reads the caller's layout itself and scales every tile by its own max |x|:
-  // no layout conversion, no input amax pass (stem_patch_kernel.h).
-  const bool patch_stem = pool_fused && m->stem_patch && H2 % 16 == 0 && W2 % 16 == 0;
+  // The patch stem (fp16x3) reads the caller's layout itself, scales every tile by its own max |x|
+  // and max-pools in its epilogue: no layout conversion, no input amax pass, no max-pool launch
+  // (stem_patch_kernel.h).
+  const bool patch_stem = h3 && m->stem_patch && H2 % 16 == 0 && W2 % 16 == 0;
   const float* xin = x;
   if (patch_stem) {
   } else if (in_layout != SFA_IN_NHWC4) {
@@ -803,37 +714,25 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   } else if (h3) {
     SFA_RC(launch_amax_nhwc4(x, B, H, W, AM(AM_INPUT), st));
   }
-  // stem conv7x7/s2/p3 + BN + ReLU   (fpn_resnet.py:179-181)
-  // fp16x3 with an 8x16-tileable stem output: the max-pool (:182) runs in the stem's epilogue.
-  // Patch stem (default): every pooled cell has one owner tile, the neighbours' parts of the
-  // tile-border cells go through a side buffer and a merge pass (no memset, no atomics).
-  // Implicit-GEMM stem (SFA_STEM_PATCH=0) and the patch stem's A/B form
-  // (SFA_STEM_PATCH_ATOMIC=1): pooled buffer zeroed, border cells combined with atomicMax.
+  // stem conv7x7/s2/p3 + BN + ReLU (fpn_resnet.py:179-181) + max-pool (:182): the patch stem owns
+  // every pooled cell once, the neighbours' parts of the tile-border cells go through a side
+  // buffer and a merge pass (no memset, no atomics); otherwise the conv and the max-pool kernel.
   {
-    ConvArgs a = conv_args(wb, p.stem, B, H2, W2, pool_fused ? F(bf.p0) : F(bf.s0), nullptr, 1);
+    ConvArgs a = conv_args(wb, p.stem, B, H2, W2, patch_stem ? F(bf.p0) : F(bf.s0), nullptr, 1);
     a.seg[0] = seg(xin, B, H, W, 4, 7, 2, 3);  // the patch stem reads NCHW3 planes through it too
     io(a, AM_INPUT, -1, AM_STEM);
     if (patch_stem) {
       a.amax_in[0] = nullptr;  // per-tile scales
       a.stem_in = in_layout == SFA_IN_NHWC4 ? STEM_IN_NHWC4
                                              : (in_layout == SFA_IN_NCHW3_FLIP_HW ? STEM_IN_NCHW3_FLIP : STEM_IN_NCHW3);
-      if (m->stem_atomic) {
-        a.part = nullptr;
-        a.part_floats = 0;
-        SFA_HIP_TRY(hipMemsetAsync(F(bf.p0), 0, (size_t)B * (H2 / 2) * (W2 / 2) * 64 * sizeof(float), st));
-      } else {
-        a.part = F(bf.s0);  // the (here unused) unfused stem buffer
-        a.part_floats = (size_t)B * H2 * W2 * 64;
-      }
-      SFA_RC(launch_stem_patch(tuned(a, m), st));
-    } else if (pool_fused) {
-      SFA_HIP_TRY(hipMemsetAsync(F(bf.p0), 0, (size_t)B * (H2 / 2) * (W2 / 2) * 64 * sizeof(float), st));
-      SFA_RC(launch_conv(tuned(a, m), EPI_POOL, m->math, st));
+      a.part = F(bf.s0);  // the (here unused) unfused stem buffer
+      a.part_floats = (size_t)B * H2 * W2 * 64;
+      SFA_RC(launch_stem_patch(a, st));
     } else {
-      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
+      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
   }
-  if (!pool_fused) SFA_RC(launch_maxpool3s2(F(bf.s0), F(bf.p0), B, H2, W2, 64, st));  // :182
+  if (!patch_stem) SFA_RC(launch_maxpool3s2(F(bf.s0), F(bf.p0), B, H2, W2, 64, st));  // :182
   // residual layers (fpn_resnet.py:184-187)
   const float* xcur = F(bf.p0);
   int xslot = AM_STEM;  // maxpool keeps the stem's max
@@ -850,7 +749,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       ConvArgs a = conv_args(wb, p.blk[li][0][0], B, oh, ow, t, nullptr, 1);
       a.seg[0] = seg(xcur, B, h, w, cin, 3, stride, 1);
       io(a, xslot, -1, blk_slot(li, 0, 0));
-      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
+      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     {
       ConvArgs a = conv_args(wb, p.blk[li][0][1], B, oh, ow, av, li == 0 ? xcur : nullptr, 1);
@@ -861,20 +760,20 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
         a.seg[1] = seg(xcur, B, h, w, cin, 1, stride, 0);
       }
       io(a, blk_slot(li, 0, 0), li > 0 ? xslot : -1, blk_slot(li, 0, 1));
-      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
+      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     // block 1
     {
       ConvArgs a = conv_args(wb, p.blk[li][1][0], B, oh, ow, t, nullptr, 1);
       a.seg[0] = seg(av, B, oh, ow, planes, 3, 1, 1);
       io(a, blk_slot(li, 0, 1), -1, blk_slot(li, 1, 0));
-      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
+      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     {
       ConvArgs a = conv_args(wb, p.blk[li][1][1], B, oh, ow, lv, av, 1);
       a.seg[0] = seg(t, B, oh, ow, planes, 3, 1, 1);
       io(a, blk_slot(li, 1, 0), -1, blk_slot(li, 1, 1));
-      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
+      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     xcur = lv;
     xslot = blk_slot(li, 1, 1);
@@ -904,7 +803,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       a.wk0 = 0;
       a.seg[0] = seg(x, B, xh, xw, xc, 1, 1, 0);
       io(a, xslot_in, -1, -1);
-      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, fs));
+      SFA_RC(launch_conv(a, EPI_STD, m->math, fs));
     }
     ConvArgs a = conv_args(wb, pc, B, 2 * xh, 2 * xw, out, nullptr, 0);
     a.Kpad = sc;
@@ -915,7 +814,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.res_sh = xh > 1 ? (float)(xh - 1) / (float)(2 * xh - 1) : 0.f;
     a.res_sw = xw > 1 ? (float)(xw - 1) / (float)(2 * xw - 1) : 0.f;
     io(a, skip_slot, -1, out_slot);
-    return launch_conv(tuned(a, m), EPI_STD, m->math, fs);
+    return launch_conv(a, EPI_STD, m->math, fs);
   };
   if (commute_at(0)) {
     SFA_RC(fpn_pair(0, F(bf.l[3]), H / 32, W / 32, 512, blk_slot(3, 1, 1), F(bf.l[2]), 256, blk_slot(2, 1, 1),
@@ -929,7 +828,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       a.seg[0] = seg(F(bf.up1), B, H16, W16, 512, 1, 1, 0);
       a.seg[1] = seg(F(bf.l[2]), B, H16, W16, 256, 1, 1, 0);
       io(a, blk_slot(3, 1, 1), blk_slot(2, 1, 1), AM_FPN + 0);  // up1 = upsample(layer4)
-      SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
+      SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
   }
   SFA_RC(launch_upsample2x(F(bf.c1), F(bf.up2), B, H16, W16, 256, st));
@@ -969,7 +868,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       a.hoff[j] = hoff[j];
     }
     a.hout = lout[f];
-    return tuned(a, m);
+    return a;
   };
   auto probing = [&](hipStream_t hs) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
@@ -981,37 +880,17 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     if (probe) SFA_HIP_TRY(hipEventRecord(m->probe_ev[2 * f], hs));
     SFA_RC(launch_conv(head_args(f), EPI_HEAD, m->math, hs));
     if (probe) SFA_HIP_TRY(hipEventRecord(m->probe_ev[2 * f + 1], hs));
-    if (probe) const_cast<sfa_model*>(m)->probe_grouped = false;
-    return SFA_OK;
-  };
-  // all three levels in one launch (SFA_OPT_HEADS_GROUPED), or per level when the math mode /
-  // A/B head kernel has no grouped form
-  auto launch_heads_grouped = [&](hipStream_t hs) -> int {
-    const ConvArgs lv[3] = {head_args(0), head_args(1), head_args(2)};
-    const bool probe = probing(hs);
-    if (probe) SFA_HIP_TRY(hipEventRecord(m->probe_ev[0], hs));
-    const int rc = launch_conv_heads_group(lv, 3, m->math, hs);
-    if (rc == SFA_E_UNSUPPORTED) {
-      SFA_RC(launch_head(0, hs));
-      SFA_RC(launch_head(1, hs));
-      return launch_head(2, hs);
-    }
-    SFA_RC(rc);
-    if (probe) SFA_HIP_TRY(hipEventRecord(m->probe_ev[1], hs));
-    if (probe) const_cast<sfa_model*>(m)->probe_grouped = true;
     return SFA_OK;
   };
   // (m->side is read under fork_mu below, as the overlap decision)
   // level 0 needs only up_level2: fork it onto the side stream (graph capture follows
   // the event edges), join before apply_kfpn
-  // m->side / m->side2 are read under fork_mu: sfa_model_set_side_streams destroys them under
-  // the same lock, so a concurrent call cannot pull a stream out from under this forward
+  // m->side is read under fork_mu: sfa_model_set_side_streams destroys it under the same lock,
+  // so a concurrent call cannot pull a stream out from under this forward
   std::unique_lock<std::mutex> fork_lock(const_cast<sfa_model*>(m)->fork_mu);
   int sdev = -1;
-  const bool grouped = m->heads_grouped == 1 || (m->heads_grouped == 2 && !m->side);
-  const bool overlap = m->side && !grouped && !(m->probe & SFA_PROBE_SERIAL) &&
+  const bool overlap = m->side && !(m->probe & SFA_PROBE_SERIAL) &&
                        hipStreamGetDevice(st, &sdev) == hipSuccess && sdev == m->device;
-  const bool side2_on = overlap && m->side2 && m->fpn3_side;
   if (overlap) {
     SFA_HIP_TRY(hipEventRecord(m->fork, st));
     SFA_HIP_TRY(hipStreamWaitEvent(m->side, m->fork, 0));
@@ -1019,13 +898,8 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   // Everything between the fork and the join: any failure inside returns from this lambda
   // only, so the side stream is still joined below (a graph capture stays valid, no work is
   // left orphaned on the side stream).
-  bool side2_forked = false;  // side2 joined this forward (graph capture: it must be joined back)
   auto forked = [&]() -> int {
-  if (overlap) {
-    SFA_RC(launch_head(0, m->side));
-  } else if (!grouped) {
-    SFA_RC(launch_head(0, st));
-  }
+  SFA_RC(launch_head(0, overlap ? m->side : st));
   if (commute_at(1)) {
     SFA_RC(fpn_pair(1, F(bf.c1), H16, W16, 256, AM_FPN + 0, F(bf.l[1]), 128, blk_slot(1, 1, 1), F(bf.c2),
                     AM_FPN + 1, st));
@@ -1037,7 +911,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.seg[0] = seg(F(bf.up2), B, H8, W8, 256, 1, 1, 0);
     a.seg[1] = seg(F(bf.l[1]), B, H8, W8, 128, 1, 1, 0);
     io(a, AM_FPN + 0, blk_slot(1, 1, 1), AM_FPN + 1);
-    SFA_RC(launch_conv(tuned(a, m), EPI_STD, m->math, st));
+    SFA_RC(launch_conv(a, EPI_STD, m->math, st));
   }
   SFA_RC(launch_upsample2x(F(bf.c2), F(bf.up3), B, H8, W8, 128, st));
   // FPN level 3 (-> up_level4) on stream fs
@@ -1051,21 +925,9 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.seg[0] = seg(F(bf.up3), B, H4, W4, 128, 1, 1, 0);
     a.seg[1] = seg(F(bf.l[0]), B, H4, W4, 64, 1, 1, 0);
     io(a, AM_FPN + 1, blk_slot(0, 1, 1), AM_FPN + 2);
-    return launch_conv(tuned(a, m), EPI_STD, m->math, fs);
+    return launch_conv(a, EPI_STD, m->math, fs);
   };
-  if (side2_on) {
-    // up_level3 is written: FPN level 3 + the level-2 heads on side2, the level-1 heads here,
-    // side by side (neither waits for the other)
-    SFA_HIP_TRY(hipEventRecord(m->mid, st));
-    SFA_HIP_TRY(hipStreamWaitEvent(m->side2, m->mid, 0));
-    side2_forked = true;
-    SFA_RC(fpn3(m->side2));
-    SFA_RC(launch_head(2, m->side2));
-    SFA_RC(launch_head(1, st));
-    return SFA_OK;
-  }
   SFA_RC(fpn3(st));
-  if (grouped) return launch_heads_grouped(st);
   // level 2 (needs up_level4, just written) on the side stream after level 0, level 1 here:
   // the two 1,444-tile launches run side by side, so neither one's last partial wave of tiles
   // leaves CUs idle
@@ -1082,10 +944,6 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   if (overlap) {  // the join, on success and on failure alike
     SFA_HIP_TRY(hipEventRecord(m->join, m->side));
     SFA_HIP_TRY(hipStreamWaitEvent(st, m->join, 0));
-    if (side2_forked) {
-      SFA_HIP_TRY(hipEventRecord(m->join2, m->side2));
-      SFA_HIP_TRY(hipStreamWaitEvent(st, m->join2, 0));
-    }
   }
   SFA_RC(frc);
   // apply_kfpn (fpn_resnet.py:248-254)

@@ -20,13 +20,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SFA_HIP_LIB", os.path.join(_HERE, "libsfa_hip.so"))
 
 SFA_OK = 0
+ABI_VERSION = 2  # include/sfa_hip.h SFA_ABI_VERSION
 SFA_MAX_HEADS = 8
 SFA_BEV_MAX_BATCH = 64
 BEV_NCHW3_F32, BEV_NCHW3_F64, BEV_NHWC4_F32 = 0, 1, 2
 BEV_RAW, BEV_PREFILTERED, BEV_FLIP_HW, BEV_FORCE_ATOMIC, BEV_FORCE_BINNED, BEV_STRIP8 = 0, 1, 2, 4, 8, 16
 # sfa_model_set_option keys (include/sfa_hip.h sfa_model_option)
-(OPT_CONV_TUNE, OPT_STEM_PATCH, OPT_STEM_POOL_FUSION, OPT_STEM_PATCH_ATOMIC, OPT_FPN_COMMUTE,
- OPT_FPN3_SIDE, OPT_STEM_ABL, OPT_HEADS_GROUPED) = range(8)
+OPT_STEM_PATCH, OPT_FPN_COMMUTE = 0, 1
+OPT_COUNT = 2  # keys 0 .. OPT_COUNT - 1
 IN_NCHW3, IN_NHWC4, IN_NCHW3_FLIP_HW = 0, 1, 2
 
 
@@ -53,7 +54,7 @@ _PROTOS = {
     "sfa_last_error_string": (ctypes.c_char_p, []),
     "sfa_bev_scratch_size": (_c_size, [_c_int]),
     "sfa_bev_voxelize": (_c_int, [_vp, ctypes.POINTER(_c_i64), _c_int, ctypes.POINTER(ctypes.c_double),
-                                  _c_int, _c_int, _vp, _vp, _vp]),
+                                  _c_int, _c_int, _vp, _vp, _c_size, _vp]),
     "sfa_filter_scratch_size": (_c_size, [_c_i64]),
     "sfa_filter_points": (_c_int, [_vp, _c_i64, ctypes.POINTER(ctypes.c_double), _vp, _vp, _vp,
                                    _c_size, _vp]),
@@ -171,7 +172,7 @@ def lib():
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.sfa_abi_version() != 1:
+    if L.sfa_abi_version() != ABI_VERSION:
         raise SfaNativeError("libsfa_hip ABI version mismatch")
     _lib = L
     return L

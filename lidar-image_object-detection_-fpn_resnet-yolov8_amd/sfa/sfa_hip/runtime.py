@@ -123,7 +123,7 @@ class KfpnEngine:
         t.set_math(self.math)
         if not self.side_streams:
             t.set_side_streams(False)
-        for key in range(_lib.OPT_STEM_ABL + 1):  # the same kernel choices
+        for key in range(_lib.OPT_COUNT):  # the same kernel choices (every option key)
             if t.get_option(key) != self.get_option(key):
                 t.set_option(key, self.get_option(key))
         return t
@@ -285,7 +285,7 @@ class BevVoxelizer:
             flags |= _lib.BEV_STRIP8
         check(lib().sfa_bev_voxelize(points.data_ptr() if points.numel() else None, offs_c, B,
                                      _boundary_arr(boundary), flags, layout, out.data_ptr(),
-                                     self.scratch.data_ptr(),
+                                     self.scratch.data_ptr(), self.scratch.numel(),
                                      stream if stream is not None else _lib.stream_ptr(self.device)),
               "sfa_bev_voxelize")
         return out

@@ -29,7 +29,7 @@ def test_library_exports_header_symbols():
     for s in syms:
         assert hasattr(L, s), f"{s} declared in include/sfa_hip.h but not exported"
     assert sorted(_lib.EXPORTED_SYMBOLS) == syms, "ctypes prototypes out of sync with the header"
-    assert L.sfa_abi_version() == 1
+    assert L.sfa_abi_version() == _lib.ABI_VERSION == 2
 
 
 def test_exported_symbols_are_only_the_abi():
@@ -173,8 +173,12 @@ def test_argument_errors_before_any_launch():
     assert L.sfa_decode(p, p, p, p, p, 1, 3, 304, 304, 50, 1, p, p, 16, None) == -1
     offs = (ctypes.c_int64 * 2)(0, 10)
     bnd = (ctypes.c_double * 6)(0, 50, -25, 25, -2.73, 1.27)
-    assert L.sfa_bev_voxelize(p, offs, 0, bnd, 0, 2, p, p, None) == -1
-    assert L.sfa_bev_voxelize(p, offs, 1, bnd, 32, 2, p, p, None) == -1  # unknown flag bit
+    big = L.sfa_bev_scratch_size(1)
+    assert L.sfa_bev_voxelize(p, offs, 0, bnd, 0, 2, p, p, big, None) == -1
+    assert L.sfa_bev_voxelize(p, offs, 1, bnd, 32, 2, p, p, big, None) == -1  # unknown flag bit
+    # a scratch smaller than the batch's layout is refused before any launch (SFA_E_WORKSPACE)
+    assert L.sfa_bev_voxelize(p, offs, 1, bnd, 0, 2, p, p, big - 1, None) == -4
+    assert b"scratch" in L.sfa_last_error_string()
     assert L.sfa_bev_scratch_size(16) == 2 * 16 * 608 * 608 * 12  # atomic-path cells + binned records
     # kernel probe (bench roofline): null model / unknown flags / reading a disabled probe
     ms = (ctypes.c_float * 3)()
@@ -190,17 +194,17 @@ def test_argument_errors_before_any_launch():
         assert L.sfa_model_probe_times(h, ms, 4) == -1
         # kernel-choice options live in the handle (no env reads on the launch path)
         v = ctypes.c_int()
-        defaults = {_lib.OPT_CONV_TUNE: 0, _lib.OPT_STEM_PATCH: 1, _lib.OPT_STEM_POOL_FUSION: 1,
-                    _lib.OPT_STEM_PATCH_ATOMIC: 0, _lib.OPT_FPN_COMMUTE: 7, _lib.OPT_FPN3_SIDE: 0,
-                    _lib.OPT_STEM_ABL: 0, _lib.OPT_HEADS_GROUPED: 0}
+        defaults = {_lib.OPT_STEM_PATCH: 1, _lib.OPT_FPN_COMMUTE: 7}
+        assert len(defaults) == _lib.OPT_COUNT
         for key, val in defaults.items():
             assert L.sfa_model_get_option(h, key, ctypes.byref(v)) == 0 and v.value == val, key
-        assert L.sfa_model_set_option(h, _lib.OPT_CONV_TUNE, 28) == 0
-        assert L.sfa_model_get_option(h, _lib.OPT_CONV_TUNE, ctypes.byref(v)) == 0 and v.value == 28
+        assert L.sfa_model_set_option(h, _lib.OPT_STEM_PATCH, 0) == 0
+        assert L.sfa_model_get_option(h, _lib.OPT_STEM_PATCH, ctypes.byref(v)) == 0 and v.value == 0
         assert L.sfa_model_set_option(h, _lib.OPT_FPN_COMMUTE, 9) == -1
-        assert L.sfa_model_set_option(h, _lib.OPT_HEADS_GROUPED, 3) == -1
-        assert L.sfa_model_set_option(h, _lib.OPT_HEADS_GROUPED, 1) == 0
-        assert L.sfa_model_get_option(h, _lib.OPT_HEADS_GROUPED, ctypes.byref(v)) == 0 and v.value == 1
+        assert L.sfa_model_set_option(h, _lib.OPT_FPN_COMMUTE, 5) == 0
+        # the round-3 A/B keys (tune bits, grouped heads, ...) are gone: unknown keys now
+        for gone in range(_lib.OPT_COUNT, 8):
+            assert L.sfa_model_set_option(h, gone, 0) == -1
         assert L.sfa_model_set_option(h, 99, 0) == -1 and b"unknown key" in L.sfa_last_error_string()
         assert L.sfa_model_get_option(h, 99, ctypes.byref(v)) == -1
         assert L.sfa_model_set_option(None, 0, 0) == -1

@@ -172,3 +172,38 @@ def test_oversized_frame_uses_atomic_path(gpu):
     assert _scratch_clean(vox)
     exp = bev_oracle.makeBEVMap(bev_oracle.get_filtered_lidar(pts, gc.BOUNDARY), gc.BOUNDARY)
     np.testing.assert_array_equal(got, exp)
+
+
+def test_scratch_shared_across_batch_sizes(gpu):
+    """One scratch (sized for 8 frames, as runtime.voxelizer() shares it) serves calls of every
+    batch size and path in any order: the layout follows the scratch's capacity, not the call's
+    batch, so a small call's records never land in a later larger call's zero areas (ADVICE r03:
+    B = 1 blocked, then B = 4 atomic / B = 2 binned / a frame over 1 M points)."""
+    from sfa_hip import synthetic
+    rng = np.random.default_rng(17)
+    huge = np.zeros((1_200_000, 4), np.float32)  # > 1024 regions of one frame: not the blocked path
+    huge[:, 0] = rng.uniform(-1, 51, huge.shape[0])
+    huge[:, 1] = rng.uniform(-26, 26, huge.shape[0])
+    huge[:, 2] = rng.uniform(-3, 1.5, huge.shape[0])
+    huge[:, 3] = rng.uniform(0, 1, huge.shape[0])
+    sweeps = [synthetic.synthetic_point_cloud(s) for s in range(20, 28)]
+    exp = {}
+
+    def oracle(c):
+        k = id(c)
+        if k not in exp:
+            exp[k] = bev_oracle.makeBEVMap(bev_oracle.get_filtered_lidar(c, gc.BOUNDARY), gc.BOUNDARY)
+        return exp[k]
+
+    vox = runtime.BevVoxelizer(gpu, 8)
+    calls = [(sweeps[:1], 0), (sweeps[1:5], _lib.BEV_FORCE_ATOMIC), (sweeps[:1], 0),
+             (sweeps[2:4], _lib.BEV_FORCE_BINNED), (sweeps[:1], _lib.BEV_STRIP8), (sweeps, 0),
+             (sweeps[:1], 0), ([sweeps[5], huge, sweeps[6]], 0), (sweeps[:2], 0),
+             ([huge], _lib.BEV_FORCE_ATOMIC), (sweeps[3:8], 0)]
+    for clouds, flags in calls:
+        offs = np.cumsum([0] + [c.shape[0] for c in clouds])
+        pts = torch.from_numpy(np.concatenate(clouds)).to(gpu)
+        got = vox(pts, offs, gc.BOUNDARY, layout=_lib.BEV_NCHW3_F64, flags=flags).cpu().numpy()
+        assert _scratch_clean(vox), (len(clouds), flags)
+        for i, c in enumerate(clouds):
+            np.testing.assert_array_equal(got[i], oracle(c), err_msg=f"B={len(clouds)} flags={flags} frame {i}")

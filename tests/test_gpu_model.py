@@ -196,42 +196,6 @@ def test_forward_608_weight_seeds(gpu, seed):
         assert e <= TOL, h
 
 
-def test_stem_pool_fusion_bit_exact(golden, gpu):
-    """fp16x3 stem with the max-pool fused into its epilogue (tile-border cells combined by
-    atomicMax) == stem conv + maxpool3s2_kernel, bit for bit over the whole forward."""
-    x = torch.from_numpy(synthetic.synthetic_bev(3, 160, 192, seed=11)).to(gpu)
-    outs = []
-    for flag in (1, 0):
-        model = make_model(golden, gpu)
-        eng = model._engine(gpu)
-        eng.set_option(_lib.OPT_STEM_PATCH, 0)  # the implicit-GEMM stem (same K order as unfused)
-        eng.set_option(_lib.OPT_STEM_POOL_FUSION, flag)
-        eng.set_math(_math("fp16x3"))
-        with torch.no_grad():
-            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
-    for h in gc.HEADS:
-        np.testing.assert_array_equal(outs[0][h], outs[1][h])
-
-
-def test_stem_patch_side_buffer_bit_exact(golden, gpu):
-    """Patch stem: tile-border pooled cells through the owner tile + side buffer +
-    stem_pool_merge_kernel (default) == atomicMax into the zeroed pooled buffer
-    (OPT_STEM_PATCH_ATOMIC), bit for bit over the whole forward. 160x192 -> an 80x96 conv
-    output = 5x6 tiles of 16x16, so the up, left and up-left (corner) merges all run."""
-    x = torch.from_numpy(synthetic.synthetic_bev(3, 160, 192, seed=23)).to(gpu)
-    outs = []
-    for flag in (0, 1):
-        model = make_model(golden, gpu)
-        eng = model._engine(gpu)
-        eng.set_option(_lib.OPT_STEM_PATCH, 1)
-        eng.set_option(_lib.OPT_STEM_PATCH_ATOMIC, flag)
-        eng.set_math(_math("fp16x3"))
-        with torch.no_grad():
-            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
-    for h in gc.HEADS:
-        np.testing.assert_array_equal(outs[0][h], outs[1][h])
-
-
 @pytest.mark.parametrize("hw", [(160, 192), (608, 608)])
 def test_stem_patch_matches_gather_stem(golden, gpu, hw):
     """fp16x3 stem + pool from LDS input patches (stem_patch_kernel.h: K laid out with kw
@@ -280,128 +244,12 @@ def test_fpn_commute_matches_concat_conv(golden, gpu):
         assert float(np.max(np.abs(outs[0][h] - r) / scale)) <= 1e-4, h
 
 
-@pytest.mark.parametrize("hw", [(160, 192), (96, 96)])
-def test_round2_kernels_match_round1(golden, gpu, hw):
-    """Round-2 conv kernels (conv_r3_kernel for the heads and the big-M non-strip convs, the
-    transposed / pre-split strip kernel) == the round-1 kernels (OPT_CONV_TUNE 28: conv_h3_kernel,
-    the plain strip kernel) to f32 rounding (the head epilogue sums the 1x1 conv in another
-    order), both within the 1e-4 bar of the CPU reference. Odd sizes: partial last row tiles,
-    tiles spanning two frames, every image border of the register-A loads."""
-    from oracle import model_oracle
-    x = torch.from_numpy(synthetic.synthetic_bev(3, hw[0], hw[1], seed=29)).to(gpu)
-    outs = []
-    for flag in (0, 28):
-        model = make_model(golden, gpu)
-        model._engine(gpu).set_option(_lib.OPT_CONV_TUNE, flag)
-        model._engine(gpu).set_math(_math("fp16x3"))
-        with torch.no_grad():
-            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
-    sd = gc.state_dict_np(golden.model)
-    ref = model_oracle.forward(model_oracle.state_dict_torch(sd), x.cpu(), dict(gc.HEADS))
-    for h in gc.HEADS:
-        r = ref[h].numpy()
-        scale = np.maximum(1.0, np.abs(r))
-        d = float(np.max(np.abs(outs[0][h] - outs[1][h]) / scale))
-        e = float(np.max(np.abs(outs[0][h] - r) / scale))
-        print(f"round-2 vs round-1 kernels {hw} {h}: {d:.3g}, vs reference {e:.3g}")
-        assert d <= 2e-5, h
-        assert e <= 1e-4, h
-
-
-@pytest.mark.parametrize("hw", [(160, 192), (96, 96), (608, 608)])
-def test_heads_stagger_bit_identical(golden, gpu, hw):
-    """The heads conv with waves 4-7 half a K-tile behind their SIMD partners (three W stages, the
-    default; OPT_CONV_TUNE bit 131072 without the second half's s_setprio; bit 16777216 with the
-    taps kw 1, 2 shifted by DPP from the previous tap's fragments) adds the same products in the
-    same order as the unstaggered kernel (bit 65536): bit-identical outputs. Odd sizes
-    cover partial tiles; K-tile counts 18 / 36 / 72 (C = 64 / 128 / 256) both parities."""
-    x = torch.from_numpy(synthetic.synthetic_bev(2, hw[0], hw[1], seed=37)).to(gpu)
-    outs = []
-    for flag in (0, 65536, 131072, 16777216, 33554432):
-        model = make_model(golden, gpu)
-        model._engine(gpu).set_option(_lib.OPT_CONV_TUNE, flag)
-        model._engine(gpu).set_math(_math("fp16x3"))
-        with torch.no_grad():
-            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
-    for h in gc.HEADS:
-        np.testing.assert_array_equal(outs[1][h], outs[0][h], err_msg=h)
-        np.testing.assert_array_equal(outs[2][h], outs[0][h], err_msg=h)
-        np.testing.assert_array_equal(outs[3][h], outs[0][h], err_msg=f"{h}: shifted A (tune 16777216)")
-        np.testing.assert_array_equal(outs[4][h], outs[0][h], err_msg=f"{h}: 192-row level-0 tiles (tune 33554432)")
-
-
-@pytest.mark.parametrize("hw", [(160, 192), (96, 96), (608, 608)])
-def test_heads_grouped_bit_identical(golden, gpu, hw):
-    """The three levels' heads as ONE launch (SFA_OPT_HEADS_GROUPED: conv_r3_group_kernel, level
-    tiles ordered by K, padding blocks) give the per-level launches' bits: every tile runs the
-    same body on the same arguments. With a per-level A/B head kernel (tune 65536) the grouped
-    option falls back to per-level launches, same bits again."""
-    x = torch.from_numpy(synthetic.synthetic_bev(2, hw[0], hw[1], seed=43)).to(gpu)
-    outs = []
-    for grouped, tune in ((0, 0), (1, 0), (1, 65536)):
-        model = make_model(golden, gpu)
-        eng = model._engine(gpu)
-        eng.set_option(_lib.OPT_CONV_TUNE, tune)
-        eng.set_option(_lib.OPT_HEADS_GROUPED, grouped)
-        eng.set_math(_math("fp16x3"))
-        with torch.no_grad():
-            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
-    for h in gc.HEADS:
-        np.testing.assert_array_equal(outs[1][h], outs[0][h], err_msg=h)
-        np.testing.assert_array_equal(outs[2][h], outs[0][h], err_msg=h)
-
-
-@pytest.mark.parametrize("tune", [2097152, 8388608])
-def test_strip256_bit_identical(golden, gpu, tune):
-    """256 x 128 strip tiles (one 8-wave block per CU) for the 256- / 128-wide body convs: every
-    output element runs the same K loop (super-steps kh x chunk, then kw) as in the 128 x 128
-    tiles, so the bits equal the default's (608 x 608: the bench's geometry picks these tiles)."""
-    x = torch.from_numpy(synthetic.synthetic_bev(2, 608, 608, seed=53)).to(gpu)
-    outs = []
-    for t in (0, tune):
-        model = make_model(golden, gpu)
-        model._engine(gpu).set_option(_lib.OPT_CONV_TUNE, t)
-        model._engine(gpu).set_math(_math("fp16x3"))
-        with torch.no_grad():
-            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
-    for h in gc.HEADS:
-        np.testing.assert_array_equal(outs[1][h], outs[0][h], err_msg=h)
-
-
-def test_head_probe_grouped(golden, gpu):
-    """Probe with grouped heads: the one launch's duration in entry 0, zeros after it; results
-    unchanged; per-level probing again once the option is off."""
-    model = make_model(golden, gpu)
-    eng = model._engine(gpu)
-    eng.set_math(_math("fp16x3"))
-    x = torch.from_numpy(synthetic.synthetic_bev(3, 160, 192, seed=47)).to(gpu)
-    with torch.no_grad():
-        eng.set_option(_lib.OPT_HEADS_GROUPED, 0)
-        base = {h: v.cpu().numpy() for h, v in model(x).items()}
-        eng.set_option(_lib.OPT_HEADS_GROUPED, 1)
-        eng.set_probe(_lib.PROBE_HEADS | _lib.PROBE_SERIAL)
-        try:
-            probed = {h: v.cpu().numpy() for h, v in model(x).items()}
-            ms = eng.probe_times(3)
-            eng.set_option(_lib.OPT_HEADS_GROUPED, 0)
-            model(x)
-            ms_levels = eng.probe_times(3)
-        finally:
-            eng.set_probe(0)
-    assert ms[0] > 0 and ms[1] == 0 and ms[2] == 0, ms
-    assert all(t > 0 for t in ms_levels), ms_levels
-    for h in gc.HEADS:
-        np.testing.assert_array_equal(base[h], probed[h], err_msg=h)
-
-
-@pytest.mark.parametrize("tune", [0, 28, 32, 256, 512, 65536])
-def test_batch_invariance_608(golden, gpu, tune):
+def test_batch_invariance_608(golden, gpu):
     """At the full 608x608 size (every kernel path of the bench: r3 heads, strip convs, FPN skip
     convs, r3 body convs (M >= 50000 needs >= 9 frames), split-K layer4): frames 7, 8 of a batch
     of 10 == the same frames as a batch of 2 (their rows sit at other offsets within the tiles),
     and a repeated forward is bit-identical (no cross-frame leakage, no nondeterminism)."""
     model = make_model(golden, gpu)
-    model._engine(gpu).set_option(_lib.OPT_CONV_TUNE, tune)
     model._engine(gpu).set_math(_math("fp16x3"))
     x = torch.from_numpy(synthetic.synthetic_bev(10, 608, 608, seed=31)).to(gpu)
     with torch.no_grad():
@@ -458,25 +306,6 @@ def test_side_streams_off_on_bit_exact(golden, gpu):
         np.testing.assert_array_equal(base[h], on[h], err_msg=f"{h}: forward after re-creating them differs")
 
 
-@pytest.mark.parametrize("prio", ["1", "-1"])
-def test_side_stream_priority_bit_exact(golden, gpu, monkeypatch, prio):
-    """SFA_SIDE_PRIO (read when the model is created: its side streams at the device's lowest /
-    highest priority; an A/B knob) changes only scheduling: the same bits as the default."""
-    x = torch.from_numpy(synthetic.synthetic_bev(3, 160, 192, seed=59)).to(gpu)
-    outs = []
-    for env in (None, prio):
-        if env is None:
-            monkeypatch.delenv("SFA_SIDE_PRIO", raising=False)
-        else:
-            monkeypatch.setenv("SFA_SIDE_PRIO", env)
-        model = make_model(golden, gpu)
-        model._engine(gpu).set_math(_math("fp16x3"))
-        with torch.no_grad():
-            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
-    for h in gc.HEADS:
-        np.testing.assert_array_equal(outs[1][h], outs[0][h], err_msg=h)
-
-
 @pytest.mark.parametrize("hw", [(160, 192), (608, 608)])
 def test_stem_input_layouts_bit_exact(golden, gpu, hw):
     """The patch stem reads the caller's layout itself (no conversion pass): NCHW3 (the
@@ -509,78 +338,29 @@ def test_stem_input_layouts_bit_exact(golden, gpu, hw):
 
 
 @pytest.mark.parametrize("hw", [(96, 96), (160, 192), (608, 608)])
-def test_stem_one_barrier_bit_identical(golden, gpu, hw):
-    """The one-barrier stem (double-buffered patches, pool from the accumulators + a row exchange,
-    waves 4-7 issuing their MFMAs first: the default) == the same with all waves in one order
-    (OPT_CONV_TUNE bit 262144) == round 3's three-barrier stem (bit 524288), bit for bit, for every
-    head; NHWC4 and flipped-NCHW3 reads through the default kernel too. Sizes with 3 x 3, 5 x 6 and 19 x 19
-    tiles per frame (frame, tile-row and tile-column borders of the pooled side buffer); 3
-    frames so a block's tiles span frames."""
+def test_stem_unaligned_input_bit_identical(golden, gpu, hw):
+    """An NCHW3 input that is not 16-B aligned (a view one float into a buffer) takes the patch
+    stem's round-3a kernel (4-B plane reads, three barriers per tile) instead of the one-barrier
+    kernel (aligned float4 column groups): the same bits for every head, flipped read too. Sizes with
+    3 x 3, 5 x 6 and 19 x 19 tiles per frame (frame, tile-row and tile-column borders of the pooled
+    side buffer); 3 frames so a block's tiles span frames."""
     x = torch.from_numpy(synthetic.synthetic_bev(3, hw[0], hw[1], seed=53)).to(gpu)
-    outs = []
-    for flag in (0, 262144, 524288):
-        model = make_model(golden, gpu)
-        eng = model._engine(gpu)
-        eng.set_option(_lib.OPT_CONV_TUNE, flag)
-        eng.set_math(_math("fp16x3"))
-        with torch.no_grad():
-            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
-            if flag == 0:
-                nhwc4 = torch.zeros((3, hw[0], hw[1], 4), dtype=torch.float32, device=gpu)
-                nhwc4[..., :3] = x.permute(0, 2, 3, 1)
-                o = eng.alloc_outputs(3, hw[0], hw[1])
-                eng.forward_into(nhwc4, o, _lib.IN_NHWC4)
-                nh = {h: v.cpu().numpy() for h, v in o.items()}
-                fl = {h: v.cpu().numpy() for h, v in
-                      model.forward_layout(torch.flip(x, [2, 3]).contiguous(), _lib.IN_NCHW3_FLIP_HW).items()}
+    buf = torch.empty(x.numel() + 1, dtype=torch.float32, device=gpu)
+    xu = buf[1:].view(x.shape)
+    xu.copy_(x)
+    assert xu.data_ptr() % 16 != 0 and xu.is_contiguous()
+    model = make_model(golden, gpu)
+    model._engine(gpu).set_math(_math("fp16x3"))
+    with torch.no_grad():
+        a = {h: v.cpu().numpy() for h, v in model(x).items()}
+        u = {h: v.cpu().numpy() for h, v in model(xu).items()}
+        xf = torch.flip(x, [2, 3]).contiguous()
+        bf = torch.empty(x.numel() + 1, dtype=torch.float32, device=gpu)
+        xfu = bf[1:].view(x.shape)
+        xfu.copy_(xf)
+        fa = {h: v.cpu().numpy() for h, v in model.forward_layout(xf, _lib.IN_NCHW3_FLIP_HW).items()}
+        fu = {h: v.cpu().numpy() for h, v in model.forward_layout(xfu, _lib.IN_NCHW3_FLIP_HW).items()}
     for h in gc.HEADS:
-        np.testing.assert_array_equal(outs[0][h], outs[2][h], err_msg=f"{h}: one-barrier vs three-barrier stem")
-        np.testing.assert_array_equal(outs[1][h], outs[2][h], err_msg=f"{h}: one-barrier, one wave order")
-        np.testing.assert_array_equal(nh[h], outs[2][h], err_msg=f"{h}: NHWC4")
-        np.testing.assert_array_equal(fl[h], outs[2][h], err_msg=f"{h}: flipped NCHW3")
-
-
-@pytest.mark.parametrize("hw", [(160, 192), (608, 608)])
-def test_fpn_residual_prefetch_bit_identical(golden, gpu, hw):
-    """FPN skip convs with the upsampled residual's taps loaded and interpolated before the K
-    loop (OPT_CONV_TUNE bit 1048576) == the default (taps in the epilogue), bit for bit."""
-    x = torch.from_numpy(synthetic.synthetic_bev(2, hw[0], hw[1], seed=59)).to(gpu)
-    outs = []
-    for flag in (0, 1048576):
-        model = make_model(golden, gpu)
-        model._engine(gpu).set_option(_lib.OPT_CONV_TUNE, flag)
-        model._engine(gpu).set_math(_math("fp16x3"))
-        with torch.no_grad():
-            outs.append({h: v.cpu().numpy() for h, v in model(x).items()})
-    for h in gc.HEADS:
-        np.testing.assert_array_equal(outs[1][h], outs[0][h], err_msg=h)
-
-
-def test_split_k_in_kernel_combine(golden, gpu):
-    """Experimental in-kernel split-K (OPT_CONV_TUNE bit 1024: the last slice to arrive adds the
-    others' partials in slice order) is bit-identical to the same split through the separate
-    reduce launch (the default), for forced 2- and 4-slice splits; its automatic split counts
-    (pick_ksplit) and no split agree to f32 rounding and with the reference."""
-    from oracle import model_oracle
-    x = torch.from_numpy(synthetic.synthetic_bev(3, 256, 320, seed=47)).to(gpu)
-
-    def run(tune):
-        model = make_model(golden, gpu)
-        eng = model._engine(gpu)
-        eng.set_math(_math("fp16x3"))
-        eng.set_option(_lib.OPT_CONV_TUNE, tune)
-        with torch.no_grad():
-            return {h: v.cpu().numpy() for h, v in model(x).items()}
-
-    for ks in (2, 4):
-        a, b = run((ks << 12) | 1024), run(ks << 12)
-        for h in gc.HEADS:
-            np.testing.assert_array_equal(a[h], b[h], err_msg=f"{h}: in-kernel vs reduce launch, {ks} slices")
-    auto, one = run(1024), run(1 << 12)
-    sd = gc.state_dict_np(golden.model)
-    ref = model_oracle.forward(model_oracle.state_dict_torch(sd), x.cpu(), dict(gc.HEADS))
-    for h in gc.HEADS:
-        r = ref[h].numpy()
-        scale = np.maximum(1.0, np.abs(r))
-        assert float(np.max(np.abs(auto[h] - one[h]) / scale)) <= 2e-5, h
-        assert float(np.max(np.abs(auto[h] - r) / scale)) <= 1e-4, h
+        np.testing.assert_array_equal(u[h], a[h], err_msg=f"{h}: unaligned NCHW3 input")
+        np.testing.assert_array_equal(fu[h], fa[h], err_msg=f"{h}: unaligned flipped input")
+        np.testing.assert_array_equal(fa[h], a[h], err_msg=f"{h}: flipped read")

@@ -1,6 +1,8 @@
 // Micro-benchmark of conv_mfma_kernel tile configurations on the KFPN layer
 // shapes at bs=16, 608x608 (tools only; not part of the product library).
-//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -pthread tools/convbench.hip -o tools/convbench
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -pthread -I<pkg>/csrc tools/convbench.hip -o tools/convbench
+//   (round 4: the conv_r3 / strip-kernel variants come from tools/experiments/r03, the product
+//   headers keep only the adopted kernels)
 //   ./tools/convbench [iters] [shape substring]; env SUSTAIN=<s>: also back-to-back for s seconds
 //   per candidate with the board's clock and power read mid-run (rocm-smi)
 //   ./tools/convbench [iters]
@@ -20,8 +22,8 @@
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_x6_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3_kernel.h"
-#include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3s_kernel.h"
-#include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_r3_kernel.h"
+#include "experiments/r03/conv_h3s_kernel.h"  // the round-3 variants (tune / ABL bits) live here
+#include "experiments/r03/conv_r3_kernel.h"
 #include "experiments/conv_ws_kernel.h"
 
 namespace sfa {

@@ -54,9 +54,49 @@ __device__ __forceinline__ void r3t_res_load(const ConvArgs& a, x6_f32x4 (&rv)[T
     }
 }
 
-// PRE: the residual tile (a.res) was loaded by the caller (r3t_res_load) into `pre`, so its
-// latency hid behind the MFMAs.
-template <int TM, int TN, int NT, bool RU = false, bool PRE = false>
+// STG: the wave's output tile (WM rows x BN channels) is staged in LDS (row pitch BN * 4 + 16 B:
+// conflict-free float4 writes and reads) and stored row-contiguous: each store instruction then
+// writes 64 x 16 B = whole 128-B lines (BN / 4 lanes per row) instead of 16 rows x 64 B halves.
+template <int TM, int TN, int NT>
+constexpr int r3t_stage_bytes() {
+  return (NT / 64) * (TM * 16) * (TN * 64 + 16) + 2 * (NT / 64) * 4;
+}
+
+// The upsampled half-resolution residual (a.res_up) of the lane's rows and channels, bilinear x2
+// with align_corners as res_up_sample evaluates it (4 float4 taps per lane and column block).
+template <int TM, int TN>
+__device__ __forceinline__ void r3t_res_up_load(const ConvArgs& a, x6_f32x4 (&rv)[TM][TN], int mrow0, int n0, int lane) {
+#pragma clang fp contract(off)
+  const int M = a.M, c16 = lane & 15, g = lane >> 4;
+  const int H = a.OH >> 1, W = a.OW >> 1;
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+    const int m = min(mrow0 + mi * 16 + c16, M - 1);
+    const int ow = m % a.OW, t = m / a.OW;
+    const int oh = t % a.OH, b = t / a.OH;
+    const float fy = a.res_sh * (float)oh, fx = a.res_sw * (float)ow;
+    const int y0 = (int)fy, x0 = (int)fx;
+    const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+    const float ly1 = fy - (float)y0, lx1 = fx - (float)x0;
+    const float ly0 = 1.f - ly1, lx0 = 1.f - lx1;
+    const float* r = a.res_up + (size_t)b * H * W * a.N;
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      const int n = n0 + ni * 16 + 4 * g;
+      const x6_f32x4 a00 = *reinterpret_cast<const x6_f32x4*>(r + (size_t)(y0 * W + x0) * a.N + n);
+      const x6_f32x4 a01 = *reinterpret_cast<const x6_f32x4*>(r + (size_t)(y0 * W + x1) * a.N + n);
+      const x6_f32x4 a10 = *reinterpret_cast<const x6_f32x4*>(r + (size_t)(y1 * W + x0) * a.N + n);
+      const x6_f32x4 a11 = *reinterpret_cast<const x6_f32x4*>(r + (size_t)(y1 * W + x1) * a.N + n);
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        rv[mi][ni][v] = fmaf(ly0, fmaf(lx0, a00[v], lx1 * a01[v]), ly1 * fmaf(lx0, a10[v], lx1 * a11[v]));
+    }
+  }
+}
+
+// PRE: the residual tile (a.res, or with RU the upsampled a.res_up) was loaded by the caller
+// (r3t_res_load / r3t_res_up_load) into `pre`, so its latency hid behind the MFMAs.
+template <int TM, int TN, int NT, bool RU = false, bool PRE = false, int EABL = 0, bool STG = false>
 __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
                                                  int mrow0, int m0, int n0, int lane, const float (&ainv)[TM],
                                                  const x6_f32x4 (*pre)[TN] = nullptr) {
@@ -66,9 +106,16 @@ __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&ac
   // batch it was computed in
 #pragma clang fp contract(off)
   const int M = a.M, c16 = lane & 15, g = lane >> 4;
+  constexpr int PITCH = TN * 64 + 16;  // STG: bytes per staged row
+  unsigned char* const stg = smem + (threadIdx.x >> 6) * (TM * 16) * PITCH;
   AmaxRows am(a.OH * a.OW, m0);
   x6_f32x4 rv[TM][TN];
-  if (RU && a.res_up) {
+  if (PRE && RU && a.res_up) {
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) rv[mi][ni] = pre[mi][ni];
+  } else if (RU && a.res_up) {
     const int H = a.OH >> 1, W = a.OW >> 1;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
@@ -120,14 +167,119 @@ __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&ac
         if (a.relu) t = fmaxf(t, 0.f);
         val[v] = t;
       }
-      if (m < M) {
-        *reinterpret_cast<x6_f32x4*>(a.y + (size_t)m * a.N + n) = val;
-        if (a.amax_out)
+      if constexpr (STG) {
+        *reinterpret_cast<x6_f32x4*>(stg + (mi * 16 + c16) * PITCH + (ni * 16 + 4 * g) * 4) = val;
+        if (m < M && a.amax_out && (EABL & 2) == 0)
+          am.add(a.amax_out, m, fmaxf(fmaxf(fabsf(val[0]), fabsf(val[1])), fmaxf(fabsf(val[2]), fabsf(val[3]))));
+      } else if (m < M) {
+        if constexpr ((EABL & 4) != 0)  // streaming (non-temporal) store
+          __builtin_nontemporal_store(val, reinterpret_cast<x6_f32x4*>(a.y + (size_t)m * a.N + n));
+        else if constexpr ((EABL & 1) == 0) *reinterpret_cast<x6_f32x4*>(a.y + (size_t)m * a.N + n) = val;
+        else asm volatile("" ::"v"(val));
+        if (a.amax_out && (EABL & 2) == 0)
           am.add(a.amax_out, m, fmaxf(fmaxf(fabsf(val[0]), fabsf(val[1])), fmaxf(fabsf(val[2]), fabsf(val[3]))));
       }
     }
   }
-  if (a.amax_out) amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1, reinterpret_cast<float*>(smem));
+  if constexpr (STG) {
+    // the wave's own rows only: its LDS writes are complete once lgkmcnt drains (no barrier)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    constexpr int LPR = TN * 4;        // lanes per row (16 B each)
+    constexpr int RPI = 64 / LPR;      // rows per store instruction
+    const int rr = lane / LPR, q = lane % LPR;
+#pragma unroll
+    for (int k = 0; k < TM * 16 / RPI; ++k) {
+      const int r = k * RPI + rr, m = mrow0 + r;
+      const x6_f32x4 v = *reinterpret_cast<const x6_f32x4*>(stg + r * PITCH + q * 16);
+      if (m < M) {
+        if constexpr ((EABL & 1) == 0) *reinterpret_cast<x6_f32x4*>(a.y + (size_t)m * a.N + n0 + 4 * q) = v;
+        else asm volatile("" ::"v"(v));
+      }
+    }
+  }
+  if (a.amax_out && (EABL & 2) == 0)
+    amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1,
+                               reinterpret_cast<float*>(smem + (STG ? (NT / 64) * (TM * 16) * PITCH : 0)));
+}
+
+// In-kernel split-K (a.tile_cnt, transposed accumulators). Slice tickets are drawn in arrival
+// order: the first nsplit - 1 arrivals write their partial (acc * ainv * winv, as for the reduce
+// launch) into part[kz] and publish it; the last arrival waits for those nsplit - 1 publications
+// (they are running: they drew their tickets before it) and combines, for each of its float4s,
+// part[0] + part[1] + ... in SLICE order — its own slice from registers — then + bias, + residual,
+// ReLU, exactly as splitk_reduce_kernel does (same bits), stores y and records the frame maxima.
+// The last block also resets the tile's two words (zero for the next launch). Returns true if the
+// block is done (it wrote a partial, or combined), i.e. always; the caller returns.
+template <int TM, int TN, int NT>
+__device__ __forceinline__ void r3t_splitk_combine(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
+                                                   int tile, int kz, int nsplit, int mrow0, int m0, int n0, int lane,
+                                                   const float (&ainv)[TM]) {
+#pragma clang fp contract(off)
+  const int M = a.M, c16 = lane & 15, g = lane >> 4;
+  int* flag = reinterpret_cast<int*>(smem);
+  unsigned* tk = a.tile_cnt + 2 * tile;
+  __syncthreads();  // every wave is past its last LDS read of the K loop: smem is free
+  if (threadIdx.x == 0) *flag = (int)atomicAdd(tk, 1u);
+  __syncthreads();
+  const bool last = *flag == nsplit - 1;
+  if (!last) {
+    float* part = a.part + (size_t)kz * M * a.N;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int m = mrow0 + mi * 16 + c16, n = n0 + ni * 16 + 4 * g;
+        const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(a.winv + n);
+        x6_f32x4 val;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) val[v] = acc[mi][ni][v] * ainv[mi] * cs[v];
+        if (m < M) *reinterpret_cast<x6_f32x4*>(part + (size_t)m * a.N + n) = val;
+      }
+    __threadfence();  // this thread's partial is device-visible ...
+    __syncthreads();  // ... and every thread's, before the publication
+    if (threadIdx.x == 0) atomicAdd(tk + 1, 1u);
+    return;
+  }
+  if (threadIdx.x == 0) {
+    // the other slices hold tickets, so they are resident and finish their partial without
+    // waiting on anything: the wait is bounded (the cap only guards a broken launch)
+    for (int it = 0; it < (1 << 22); ++it) {
+      if (__hip_atomic_load(tk + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)(nsplit - 1)) break;
+      __builtin_amdgcn_s_sleep(2);
+    }
+    tk[0] = 0u;
+    tk[1] = 0u;
+  }
+  __syncthreads();
+  __threadfence();  // acquire: the other slices' partials
+  AmaxRows am(a.OH * a.OW, m0);
+#pragma unroll
+  for (int ni = 0; ni < TN; ++ni) {
+    const int n = n0 + ni * 16 + 4 * g;
+    const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(a.winv + n);
+    const x6_f32x4 bn = *reinterpret_cast<const x6_f32x4*>(a.bias + n);
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = mrow0 + mi * 16 + c16;
+      if (m >= M) continue;
+      x6_f32x4 own;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) own[v] = acc[mi][ni][v] * ainv[mi] * cs[v];
+      const size_t e = (size_t)m * a.N + n;
+      x6_f32x4 sum = kz == 0 ? own : *reinterpret_cast<const x6_f32x4*>(a.part + e);
+      for (int z = 1; z < nsplit; ++z)
+        sum += z == kz ? own : *reinterpret_cast<const x6_f32x4*>(a.part + (size_t)z * M * a.N + e);
+      sum += bn;
+      if (a.res) sum += *reinterpret_cast<const x6_f32x4*>(a.res + e);
+      if (a.relu) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) sum[v] = fmaxf(sum[v], 0.f);
+      }
+      *reinterpret_cast<x6_f32x4*>(a.y + e) = sum;
+      if (a.amax_out) am.add(a.amax_out, m, fmaxf(fmaxf(fabsf(sum[0]), fabsf(sum[1])), fmaxf(fabsf(sum[2]), fabsf(sum[3]))));
+    }
+  }
+  if (a.amax_out) amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1, reinterpret_cast<float*>(smem + 16));
 }
 
 // Heads (EPI_HEAD, transposed form): per head and pixel, ReLU(conv3x3 + b) of the lane's 16 of
@@ -250,50 +402,59 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
   }
 }
 
-// ABL: the product form's bits (round 4: the measured-and-rejected variants and ablations —
-// compiler-scheduled DMA, A split one tile ahead, staggered split, 3-stage ring without the
-// stagger, in-kernel split-K, non-temporal stores, residual prefetch, shifted A fragments, the
-// grouped head launch — live in tools/experiments/r03/conv_r3_kernel.h with their convbench
-// hooks). The values are kept from round 3, so the instances keep their names (conv.hip R3_*).
-// Always set: 256 = spread the W DMA: A loads at block 0, then one W piece per block from block 2,
-// the two waves of a SIMD (w, w + NW/2) on alternate blocks, so no SIMD issues two DMA bursts at
-// once; 2048 = transposed accumulators (W fragment as the MFMA A operand) with the float4 /
-// shuffle epilogues above.
-// Per launch configuration:
-// 4 = s_setprio 1 for the second half of the waves,
-// 4096 = fp16 split in 2 VALU per value (split2h_x8, inline v_fma_mix),
-// 8192 = W fragments read 3 column blocks ahead (with the stagger) instead of 2,
+// ABL (tools/convbench variants): 1 = no W DMA in the K loop (ablation), 4 = s_setprio 1 for the
+// second half of the waves, 8 = do not pin the DMA / A-load placement (compiler scheduling; the
+// end-of-tile wait is then vmcnt(0), since the W DMAs are no longer known to precede the A loads),
+// 16 = split the next tile's A during this tile's MFMAs (hf / hn double buffer, +16 VGPRs),
+// 32 = pure MFMA stream (no loads, split, W reads or barriers in the K loop: the ceiling),
+// 64 = no split in the K loop (A loads kept live), 128 = no barrier in the K loop (ablations),
+// 1024 = no epilogue (accumulators kept live; ablation of the epilogue cost),
+// 262144 = (with 2048, standard epilogue) non-temporal output stores,
+// 131072 = no A loads in the K loop (with 256; ablation of the A-operand cost),
+// 65536 = (heads, with 2048) packed epilogue: v_pk_fma_f32 over channel pairs, only the head's
+// ch outputs formed,
+// 32768 = (with 2048) the epilogue also takes an upsampled half-resolution residual (a.res_up:
+// the FPN skip convs; only those instances carry its registers),
 // 16384 = scalar tap decode + per-lane tap validity masks for the A addresses (one segment,
 // C >= 32, checked at launch),
-// 32768 = the epilogue also takes an upsampled half-resolution residual (a.res_up: the FPN skip
-// convs; only those instances carry its registers),
-// 65536 = (heads) packed epilogue: v_pk_fma_f32 over channel pairs, only the head's ch outputs
-// formed,
-// 524288 = channel-chunk-major K order over segment 0 (a 3x3 window, C % 32 == 0): K-tile kt covers
-// tap kt % 9 of the 32-channel chunk kt / 9 (weight columns tap * C + 32 chunk .. +31), so the
-// blocks resident on one XCD sweep a 32-channel slice of their input window through all 9 taps
-// before the next slice: that slice (~1-2 MB per XCD for the heads) stays in the 4 MB L2, where
-// the tap-major order's whole-window working set (4-9 MB per XCD at C = 128 / 256) re-read the
-// input from the fabric at every tap (heads L0 / L1: 7x / 5x their input in HBM traffic),
-// 1048576 = half-tile stagger (NSTAGE 3): waves NW/2 .. NW - 1 run their K loop half a K-tile
-// behind their SIMD partners (w - NW/2). The barrier that closes interval i (W of tile i + 1
-// landed) comes after tile i for the first half of the waves and after the first half of tile i
-// for the second, so the partners never reach their split VALU, their tile-top W reads and the
-// barrier wait together: while one waits or splits, the other issues MFMAs. Interval i reads
-// tiles i - 1 (second half only) and i, and DMAs tile i + 1: three stages. The delayed half reads
-// the next tile's first W blocks ahead across its tile boundary (that tile was published by the
-// barrier before); the leading half reads them after its barrier. Same products in the same
-// order: bit-identical to the unstaggered loop.
-// Without the stagger the ring has two stages (NSTAGE 2).
+// 8192 = W fragments read 3 column blocks ahead (4-slot ring, NSTAGE 2) instead of 2,
+// 524288 = channel-chunk-major K order over segment 0 (a 3x3 window, C % 32 == 0): K-tile kt covers tap kt % 9 of
+// the 32-channel chunk kt / 9 (weight columns tap * C + 32 chunk .. +31), so the blocks resident
+// on one XCD sweep a 32-channel slice of their input window through all 9 taps before the next
+// slice: that slice (~1-2 MB per XCD for the heads) stays in the 4 MB L2, where the tap-major
+// order's whole-window working set (4-9 MB per XCD at C = 128 / 256) re-read the input from
+// the fabric at every tap (heads L0 / L1: 7x / 5x their input in HBM traffic),
+// 2048 = transposed accumulators (W fragment as the MFMA A operand) with the float4 / shuffle
+// epilogues above, 4096 = fp16 split in 2 VALU per value (split2h_x8, inline v_fma_mix),
+// 256 = spread the W DMA: A loads at block 0, then one W piece per block from block 2, the two
+// waves of a SIMD (w, w + NW/2) on alternate blocks, so no SIMD issues two DMA bursts at once,
+// 512 = staggered split: waves w < NW/2 split the next tile's A at block SPLIT_AT (into hn),
+// the others at the top of their tile, so after a barrier one wave of each SIMD issues MFMAs
+// while its partner splits,
+// 1048576 = half-tile stagger (NSTAGE 3, with 256 and 2048): waves NW/2 .. NW - 1 run their K
+// loop half a K-tile behind their SIMD partners (w - NW/2). The barrier that closes interval i
+// (W of tile i + 1 landed) comes after tile i for the first half of the waves and after the
+// first half of tile i for the second, so the partners never reach their split VALU, their
+// tile-top W reads and the barrier wait together: while one waits or splits, the other issues
+// MFMAs. Interval i reads tiles i - 1 (second half only) and i, and DMAs tile i + 1: three
+// stages. The delayed half reads the next tile's first W blocks ahead across its tile boundary
+// (that tile was published by the barrier before); the leading half reads them after its
+// barrier. Same products in the same order: bit-identical to the unstaggered loop.
+// 8388608 = (with the stagger, scalar taps and the chunk-major order; one segment, stride 1)
+// shifted A: the K-tile of tap (kh, kw + 1) holds, for output row m, the input pixel that tap
+// (kh, kw) held for row m + 1 (same image row), so for kw 1, 2 the lane takes its fragment from
+// its row-group neighbour by DPP (row_shl:1; lane 15 from the next sub-tile's lane 0 by
+// row_shr:15) instead of loading it, and only the lanes whose rule breaks load: row 15 of the
+// wave's last sub-tile (its neighbour is the next wave's row) and rows at the image's right edge
+// (the neighbour is the next image row). Same fragments: bit-identical.
 // The kernel body for output tile (and split-K slice) lbid; conv_r3_kernel maps blockIdx to lbid
-// with xcd_remap.
+// with xcd_remap, conv_r3_group_kernel (grouped head launch) per level.
 template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int NSEG, int ABL = 0>
 __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
+  static_assert(NSTAGE == 2 || NSTAGE == 3, "W ring depth");
   constexpr bool STAG = (ABL & 1048576) != 0;
-  static_assert((ABL & (256 | 2048)) == (256 | 2048) &&
-                    (ABL & ~(4 | 256 | 2048 | 4096 | 8192 | 16384 | 32768 | 65536 | 524288 | 1048576)) == 0,
-                "product conv_r3 form (see the bit list)");
-  static_assert(STAG ? NSTAGE == 3 : NSTAGE == 2, "W ring depth: 3 stages with the stagger, else 2");
+  static_assert(!STAG || (NSTAGE == 3 && (ABL & 256) != 0 && (ABL & 2048) != 0 && (ABL & (8 | 16 | 32 | 64 | 128 | 512)) == 0),
+                "stagger: NSTAGE 3, spread W DMA, transposed accumulators, no split / schedule ablations");
   static_assert(NSEG == 1 || NSEG == 2, "segments");
   static_assert(EPI == EPI_STD || EPI == EPI_HEAD, "epilogue");
   constexpr int NW = BM / WM, NT = NW * 64;
@@ -393,6 +554,15 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   };
 
   unsigned vmask[TM], abase[TM];
+  constexpr bool SHIFT_A = (ABL & 8388608) != 0 && FAST_A && CMAJ && STAG;
+  unsigned fixa = 0;  // SHIFT_A: bit mi = this lane's row of sub-tile mi loads its shifted fragment itself
+  if constexpr (SHIFT_A) {
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = m0 + wave * WM + mi * 16 + c16;
+      if ((m % a.OW) == a.OW - 1 || (mi == TM - 1 && c16 == 15)) fixa |= 1u << mi;
+    }
+  }
   if constexpr (FAST_A) {
     const ConvSeg& sg0 = a.seg[0];
 #pragma unroll
@@ -419,6 +589,35 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
       const unsigned off = ok ? abase[mi] + toff : 0x80000000u;
       raw[mi][0] = __builtin_amdgcn_raw_buffer_load_b128(rs0, off, 0, 0);
       raw[mi][1] = __builtin_amdgcn_raw_buffer_load_b128(rs0, off + 16u, 0, 0);
+    }
+  };
+  // SHIFT_A: the fragments of the next K-tile (tap kw > 0 of the same kh and chunk) from this
+  // tile's (still in raw: split at the top of the tile) by DPP, then the fix-up lanes' loads
+  auto shift_a = [&](int k0) {
+    constexpr int SHL1 = 0x101, SHR15 = 0x11F;  // DPP row_shl:1, row_shr:15 (rows of 16 lanes)
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          int nx = (int)raw[mi][h][v];
+          if (mi + 1 < TM)  // lane 15 of each row: lane 0 of the next sub-tile
+            nx = __builtin_amdgcn_update_dpp((int)raw[mi + 1][h][v], (int)raw[mi + 1][h][v], SHR15, 0xf, 0xf, false);
+          raw[mi][h][v] = (unsigned)__builtin_amdgcn_update_dpp(nx, (int)raw[mi][h][v], SHL1, 0xf, 0xf, false);
+        }
+    const ConvSeg& sg0 = a.seg[0];
+    const int tap = k0 >> sg0.logC, c0 = k0 & (sg0.C - 1);
+    const int kh = (tap * sg0.kdiv_mul) >> sg0.kdiv_sh, kw = tap - kh * sg0.KW;
+    const unsigned toff = (unsigned)((((kh * sg0.W + kw) << sg0.logC) + c0) << 2);
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      if ((fixa >> mi) & 1u) {
+        const bool ok = tap < 32 && ((vmask[mi] >> tap) & 1u);
+        const unsigned off = ok ? abase[mi] + toff : 0x80000000u;
+        raw[mi][0] = __builtin_amdgcn_raw_buffer_load_b128(rs0, off, 0, 0);
+        raw[mi][1] = __builtin_amdgcn_raw_buffer_load_b128(rs0, off + 16u, 0, 0);
+      }
     }
   };
   auto load_a_seg = [&](auto sgc, const __amdgpu_buffer_rsrc_t rs, int kl) {
@@ -461,10 +660,16 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
           (unsigned)(wlane + boff_s[j] + 2 * kcol(kt)), 0, 0, 0);
   };
   auto load_w = [&](int kt, unsigned char* S) {
+    const int k0 = kcol(kt);
 #pragma unroll
-    for (int j = 0; j < NB; ++j) load_w_piece(j, kt, S);
+    for (int j = 0; j < NB; ++j) {
+      if (NB_REM == 0 || j < NB - 1 || wave < NB_REM)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsw, (__attribute__((address_space(3))) void*)(S + (wave + NW * j) * 1024), 16,
+            (unsigned)(wlane + boff_s[j] + 2 * k0), 0, 0, 0);
+    }
   };
-  f16x8_t hf[2][TM];  // split A of this K-tile
+  f16x8_t hf[2][TM], hn[2][TM];  // split A of this K-tile / of the next (ABL 16)
   auto split_a = [&](f16x8_t (&h)[2][TM]) {
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
@@ -480,6 +685,9 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
       }
     }
   };
+  // ABL 16: the next tile's A is split between the MFMAs of column block SPLIT_AT (into hn)
+  // instead of at the top of its own tile, so no split VALU sits between barrier and MFMAs
+  constexpr int SPLIT_AT = TN > 6 ? TN - 4 : TN - 1;
 
   f32x4_t acc[TM][TN];
 #pragma unroll
@@ -492,7 +700,7 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   const int bfo = c16 * BROW + ((g ^ swzB(c16)) << 4);  // this lane's W fragment in a block
   constexpr int RA = (ABL & 8192) != 0 ? 3 : 2;  // W fragment blocks read ahead of their MFMAs
   constexpr int RS = RA + 1;
-  static_assert(RA == 2 || STAG, "3-block read-ahead: with the stagger only");
+  static_assert(RA == 2 || NSTAGE == 2 || STAG, "3-block read-ahead: NSTAGE 2 only");
   static_assert(!STAG || (TN % RS == 0 && TN % 2 == 0 && TN / 2 > RA), "stagger: W ring slots must repeat per tile");
   f16x8_t bq[RS][2];  // W fragment ring: block p in slot p % RS
   auto read_b = [&](const unsigned char* S, int ni, f16x8_t (&dst)[2]) {
@@ -503,12 +711,28 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   const int nk = a.Kpad / BK / nsplit;  // this block's K-tiles: kt0 .. kt0 + nk - 1
   const int kt0 = kz * nk;
   constexpr int NA_OPS = 2 * TM;  // A loads per K-tile (issued after the tile's W DMA)
-  // prologue: W tile 0 (the stagger's first interval DMAs tile 1), A tile 0; this wave's W
-  // landed, then everyone's
-  if (nk > 0) load_w(kt0, smem);
+  // prologue: W tiles 0 .. NSTAGE-2, A tile 0; this wave's W landed, then everyone's
+#pragma unroll
+  for (int p = 0; p < (STAG ? NSTAGE - 2 : NSTAGE - 1); ++p)
+    if (p < nk) load_w(kt0 + p, smem + p * STAGE);
   load_a(kt0);
+  // RUP (4194304, with 32768): the upsampled residual's taps loaded and interpolated before the
+  // K loop (one latency with the first tiles' loads instead of one more after the MFMAs)
+  constexpr bool RUP = (ABL & 4194304) != 0 && (ABL & 32768) != 0 && (ABL & 2048) != 0 && EPI == EPI_STD;
+  x6_f32x4 rup[RUP ? TM : 1][RUP ? TN : 1];
+  if constexpr (RUP) {
+    if (a.res_up) r3t_res_up_load<TM, TN>(a, rup, m0 + wave * WM, n0, lane);
+  }
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA_OPS) : "memory");
   __builtin_amdgcn_s_barrier();
+  if constexpr ((ABL & 48) != 0) split_a(hf);
+  if constexpr ((ABL & 512) != 0) {
+    if (wave >= NW / 2 ? 0 : 1) split_a(hf);
+  }
+  if constexpr (NSTAGE == 3 && !STAG) {
+    read_b(smem, 0, bq[0]);
+    read_b(smem, 1, bq[1]);
+  }
   if constexpr ((ABL & 4) != 0) {
     if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
   }
@@ -559,12 +783,24 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
       }
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
-        if (ni == 0 && more_a) load_a(kt0 + kt + 1);
+        if (ni == 0 && more_a && !(ABL & 131072)) {
+          if constexpr (SHIFT_A) {
+            const int kn = kt0 + kt + 1;
+            const int chunk = (kn * 7282) >> 16;
+            const int tap = kn - 9 * chunk;  // chunk-major: tap kn % 9 of chunk kn / 9
+            if (tap % 3 != 0)
+              shift_a(kcol(kn));
+            else
+              load_a(kn);
+          } else {
+            load_a(kt0 + kt + 1);
+          }
+        }
         {
           const bool late = HB && ni >= H2;                   // block in interval kt + 1
           const int r = HB ? (late ? ni - H2 : ni + H2) : ni;  // compile-time for each HB
           const int tw = late ? kt + 2 : kt + 1;               // tile DMA'd in this interval
-          if (r >= 2 && ((r - 2) & 1) == (HB ? 1 : 0) && ((r - 2) >> 1) < SLOTS && tw < nk)
+          if (r >= 2 && ((r - 2) & 1) == (HB ? 1 : 0) && ((r - 2) >> 1) < SLOTS && tw < nk && !(ABL & 1))
             dma_slot((r - 2) >> 1, kt0 + tw, smem + (late ? st_n2 : st_n1) * STAGE);
         }
         const int p = ni + RA;
@@ -588,48 +824,123 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
     else
       stag_loop(std::false_type{});
   }
-  // unstaggered loop (NSTAGE 2): PPB W pieces per issuing block; blocks 2, 4, .. for one half of
-  // the waves, 3, 5, .. for the other
-  constexpr int SLOTS2 = (TN - 2) / 2 >= 1 ? (TN - 2) / 2 : 1;
-  constexpr int PPB2 = (NB + SLOTS2 - 1) / SLOTS2;
-  static_assert(TN >= 4, "spread DMA needs 4 column blocks");
   int st_cur = 0;
   for (int kt = 0; kt < (STAG ? 0 : nk); ++kt) {
     const unsigned char* S = smem + st_cur * STAGE;
-    const int st_nx = st_cur ^ 1;  // the stage of tile kt + 1 (last read in tile kt - 1)
-    const bool more = kt + 1 < nk;
-    split_a(hf);
+    const int st_nx = st_cur + 1 == NSTAGE ? 0 : st_cur + 1;
+    const int st_w = st_cur == 0 ? NSTAGE - 1 : st_cur - 1;  // stage of tile kt + NSTAGE - 1
+    const bool more_w = (ABL & 32) == 0 && kt + NSTAGE - 1 < nk, more_a = (ABL & 32) == 0 && kt + 1 < nk;
+    if constexpr ((ABL & 512) != 0) {
+      if (wave_half) split_a(hf);
+    } else if constexpr ((ABL & 48) == 0) {
+      split_a(hf);
+    }
     // keep the W DMA below the split: hipcc's wait for the A loads would otherwise also wait
     // for DMAs issued just before it (it counts the conditional DMA path conservatively)
-    __builtin_amdgcn_sched_barrier(0);
+    if constexpr ((ABL & 8) == 0) __builtin_amdgcn_sched_barrier(0);
+    if constexpr (NSTAGE == 2) {
 #pragma unroll
-    for (int p = 0; p < RA; ++p) read_b(S, p, bq[p]);
+      for (int p = 0; p < RA; ++p) read_b(S, p, bq[p]);
+    }
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
-      if (ni == 0 && more) load_a(kt0 + kt + 1);
-      if (ni >= 2 && ((ni - 2) >> 1) * PPB2 < NB && more && wave_half == (ni & 1)) {
+      if constexpr ((ABL & 256) == 0) {
+        if (ni == 0 && more_w && !(ABL & 1)) load_w(kt0 + kt + NSTAGE - 1, smem + st_w * STAGE);
+        if (ni == (TN > 2 ? 1 : 0) && more_a) load_a(kt0 + kt + 1);
+      } else {
+        // PPB pieces per issuing block; blocks 2, 4, .. for one half of the waves, 3, 5, .. for the other
+        constexpr int SLOTS = (TN - 2) / 2 >= 1 ? (TN - 2) / 2 : 1;
+        constexpr int PPB = (NB + SLOTS - 1) / SLOTS;
+        static_assert(TN >= 4, "spread DMA needs 4 column blocks");
+        if (ni == 0 && more_a && !(ABL & 131072)) load_a(kt0 + kt + 1);
+        if (ni >= 2 && ((ni - 2) >> 1) * PPB < NB && more_w && !(ABL & 1) && wave_half == (ni & 1)) {
 #pragma unroll
-        for (int jj = 0; jj < PPB2; ++jj) {
-          const int j = ((ni - 2) >> 1) * PPB2 + jj;
-          if (j < NB) load_w_piece(j, kt0 + kt + 1, smem + st_nx * STAGE);
+          for (int jj = 0; jj < PPB; ++jj) {
+            const int j = ((ni - 2) >> 1) * PPB + jj;
+            if (j < NB) load_w_piece(j, kt0 + kt + NSTAGE - 1, smem + st_w * STAGE);
+          }
         }
       }
       const int p = ni + RA;
-      if (p < TN) read_b(S, p, bq[p % RS]);
-      mma_block(ni);
-      __builtin_amdgcn_sched_barrier(0);
+      if ((ABL & 32) != 0) {
+        asm volatile("" : "+v"(bq[p % RS][0]), "+v"(bq[p % RS][1]));
+      } else if (p < TN)
+        read_b(S, p, bq[p % RS]);
+      else if (NSTAGE == 3 && more_a)
+        read_b(smem + st_nx * STAGE, p - TN, bq[p % RS]);
+      const f16x8_t c0 = bq[ni % RS][0], c1 = bq[ni % RS][1];
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        f32x4_t cc = acc[mi][ni];
+        if constexpr ((ABL & 2048) != 0) {  // C^T: channels along the tile's rows
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[1][mi], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c1, hf[0][mi], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[0][mi], cc, 0, 0, 0);
+        } else {
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[1][mi], c0, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c1, cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(hf[0][mi], c0, cc, 0, 0, 0);
+        }
+        acc[mi][ni] = cc;
+      }
+      if constexpr ((ABL & 16) != 0 && (ABL & 64) == 0) {
+        if (ni == SPLIT_AT && more_a) split_a(hn);
+      }
+      if constexpr ((ABL & 512) != 0) {
+        if (ni == SPLIT_AT && more_a && !wave_half) split_a(hn);
+      }
+      if constexpr ((ABL & 64) != 0) {
+        if (ni == SPLIT_AT && more_a) {
+#pragma unroll
+          for (int mi = 0; mi < TM; ++mi) asm volatile("" ::"v"(raw[mi][0]), "v"(raw[mi][1]));
+        }
+      }
+      if constexpr ((ABL & 8) == 0) __builtin_amdgcn_sched_barrier(0);
     }
-    // this wave's W DMAs of tile kt + 1 and A loads have landed, then everyone's: that stage is
-    // readable, and this tile's stage is free for the next DMA
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    if constexpr ((ABL & 16) != 0 && (ABL & 64) == 0) {
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        hf[0][mi] = hn[0][mi];
+        hf[1][mi] = hn[1][mi];
+      }
+    }
+    if constexpr ((ABL & 512) != 0) {
+      if (!wave_half) {
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) {
+          hf[0][mi] = hn[0][mi];
+          hf[1][mi] = hn[1][mi];
+        }
+      }
+    }
+    if constexpr (NSTAGE == 3) {  // next tile's blocks 0, 1 into slots 0, 1
+      const f16x8_t n0a = bq[TN % 3][0], n0b = bq[TN % 3][1];
+      const f16x8_t n1a = bq[(TN + 1) % 3][0], n1b = bq[(TN + 1) % 3][1];
+      bq[0][0] = n0a;
+      bq[0][1] = n0b;
+      bq[1][0] = n1a;
+      bq[1][1] = n1b;
+    }
+    // this wave's W DMAs of tile kt + NSTAGE - 1 have landed (its A loads may still fly), then
+    // everyone's: that stage is readable, and this tile's stage is free for the next DMA
+    if constexpr ((ABL & 32) == 0) {
+      if (more_a && (ABL & (8 | 256)) == 0)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA_OPS) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if constexpr ((ABL & 128) == 0) __builtin_amdgcn_s_barrier();
+    }
     st_cur = st_nx;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float ainv[TM];
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi) ainv[mi] = 1.f / as[mi];
-  if (nsplit > 1) {  // split-K partials, transposed form: float4 per lane (the reduce launch adds them)
+  if (nsplit > 1 && (ABL & 2048) != 0 && a.tile_cnt && EPI == EPI_STD) {  // in-kernel split-K
+    r3t_splitk_combine<TM, TN, NT>(a, acc, smem, lbid, kz, nsplit, m0 + wave * WM, m0, n0, lane, ainv);
+    return;
+  }
+  if (nsplit > 1 && (ABL & 2048) != 0) {  // split-K partials, transposed form: float4 per lane
     float* part = a.part + (size_t)kz * M * a.N;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
@@ -644,11 +955,42 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
       }
     return;
   }
+  if (nsplit > 1) {  // split-K: this slice's partial sums, scaled back (the reduce adds the rest)
+    float* part = a.part + (size_t)kz * M * a.N;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const int row = mi * 16 + 4 * g + v, col = ni * 16 + c16;
+          const float si = __shfl(ainv[mi], row & 15, 64);
+          const int m = m0 + wave * WM + row, n = n0 + col;
+          if (m < M) part[(size_t)m * a.N + n] = acc[mi][ni][v] * si * a.winv[n];
+        }
+    return;
+  }
+  if constexpr ((ABL & 1024) != 0) {
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) asm volatile("" ::"v"(acc[mi][ni]));
+    return;
+  }
   __syncthreads();
-  if constexpr (EPI == EPI_HEAD)
-    r3t_epilogue_head<TM, TN, NT, BN / 64, (ABL & 65536) != 0>(a, acc, smem, m0 + wave * WM, n0, nt, tid, ainv);
-  else
-    r3t_epilogue_std<TM, TN, NT, (ABL & 32768) != 0, false>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv);
+  if constexpr ((ABL & 2048) != 0) {
+    if constexpr (EPI == EPI_HEAD)
+      r3t_epilogue_head<TM, TN, NT, BN / 64, (ABL & 65536) != 0>(a, acc, smem, m0 + wave * WM, n0, nt, tid, ainv);
+    else
+    if constexpr (RUP)
+      r3t_epilogue_std<TM, TN, NT, true, true, (ABL & 262144) ? 4 : 0>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv,
+                                                                        rup);
+    else
+      r3t_epilogue_std<TM, TN, NT, (ABL & 32768) != 0, false, (ABL & 262144) ? 4 : 0>(a, acc, smem, m0 + wave * WM, m0, n0,
+                                                                                      lane, ainv);
+  } else {
+    h3_epilogue16<BM, BN, WM, BN, TM, TN, NT, EPI, false>(a, acc, smem, m0, n0, nt, wave, 0, tid, ainv);
+  }
 }
 
 template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int NSEG, int ABL = 0>
@@ -656,17 +998,44 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_r3_kernel(const Conv
   conv_r3_body<BM, BN, WM, EPI, OCC, NSTAGE, NSEG, ABL>(a, xcd_remap(blockIdx.x, gridDim.x));
 }
 
+// Grouped head launch: the three KFPN levels' fused head convs (EPI_HEAD, one segment, no
+// split-K) in ONE grid. Per-level launches end in a partial last round of tiles: level 0's 361
+// tiles of 72 K-tiles each fill 256 CUs 1.41 times (the second round runs 105 tiles while 151
+// CUs idle), levels 1 / 2 (1,444 tiles of 36 / 18 K-tiles) 5.64 times. Here blocks
+// [0, start1) are level a0's tiles, [start1, start2) a1's, [start2, grid) a2's, the levels
+// ordered by K (longest first: the hardware dispatches blocks in order, so the long tiles start
+// first and the short ones fill the end — longest-processing-time-first list scheduling); each
+// range starts at a multiple of 8, so blockIdx % 8 is still the XCD and xcd_remap within the
+// level keeps an XCD on contiguous tiles. Padding blocks return at once. Every tile computes
+// exactly what conv_r3_kernel computes for it: bit-identical to the per-level launches.
+template <int BM, int BN, int WM, int OCC, int NSTAGE, int ABL>
+__global__ void __launch_bounds__((BM / WM) * 64, OCC)
+    conv_r3_group_kernel(const ConvArgs a0, const ConvArgs a1, const ConvArgs a2, int start1, int start2) {
+  const int b = blockIdx.x;
+  const int lvl = b < start1 ? 0 : (b < start2 ? 1 : 2);
+  const int first = lvl == 0 ? 0 : (lvl == 1 ? start1 : start2);
+  const int end = lvl == 0 ? start1 : (lvl == 1 ? start2 : (int)gridDim.x);
+  const ConvArgs& a = lvl == 0 ? a0 : (lvl == 1 ? a1 : a2);
+  const int lb = xcd_remap(b - first, end - first);
+  if (lb >= ((a.M + BM - 1) / BM) * (a.N / BN)) return;  // padding block (uniform)
+  conv_r3_body<BM, BN, WM, EPI_HEAD, OCC, NSTAGE, 1, ABL>(a, lb);
+}
+
 // Launch-time checks of one conv_r3 launch (the kernel never bounds-checks these).
 template <int BM, int BN, int EPI, int ABL>
 inline int conv_r3_check(const ConvArgs& a) {
   if (!a.wh || !a.winv || a.Kpad % 32 != 0 || (a.nseg == 2 && a.kseg1 % 32 != 0) || a.N % BN != 0 ||
-      (a.res_up && ((ABL & 32768) == 0 || a.res || a.nseg != 1))) {
+      (a.res_up && ((ABL & 32768) == 0 || (ABL & 2048) == 0 || a.res || a.nseg != 1))) {
     set_error("conv_r3: K/N not aligned to the tile, no split weights or an upsampled residual (Kpad=%d kseg1=%d N=%d)", a.Kpad,
               a.kseg1, a.N);
     return SFA_E_UNSUPPORTED;
   }
   if ((ABL & 16384) != 0 && (a.nseg != 1 || a.seg[0].C < 32 || a.seg[0].taps > 32)) {
     set_error("conv_r3: fast A addressing needs one segment with C >= 32 (C=%d)", a.seg[0].C);
+    return SFA_E_UNSUPPORTED;
+  }
+  if ((ABL & 8388608) != 0 && (a.nseg != 1 || a.seg[0].stride != 1 || a.seg[0].KW != 3 || a.OW != a.seg[0].W)) {
+    set_error("conv_r3: shifted A needs one stride-1 3x3 segment (stride=%d KW=%d)", a.seg[0].stride, a.seg[0].KW);
     return SFA_E_UNSUPPORTED;
   }
   if ((ABL & 524288) != 0 && (a.seg[0].taps != 9 || a.seg[0].C % 32 != 0 ||
@@ -715,11 +1084,44 @@ inline int launch_conv_r3_cfg(const ConvArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((conv_r3_kernel<BM, BN, WM, EPI, OCC, NSTAGE, 1, ABL>), dim3((unsigned)nblocks),
                        dim3((BM / WM) * 64), 0, st, a);
   SFA_LAUNCH_CHECK();
-  if (ks > 1) {  // the slices' partials combined by the reduce launch
+  if (ks > 1 && !((ABL & 2048) != 0 && a.tile_cnt)) {  // no in-kernel combine: the reduce launch
     const long long nel = (long long)a.M * a.N;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((nel + 1023) / 1024)), dim3(256), 0, st, a);
     SFA_LAUNCH_CHECK();
   }
+  return SFA_OK;
+}
+
+// The grouped head launch (conv_r3_group_kernel) over n = 3 levels: one segment each, no
+// split-K, EPI_HEAD; the levels are ordered by K, longest first (stable).
+template <int BM, int BN, int WM, int OCC, int NSTAGE, int ABL>
+inline int launch_conv_r3_group_cfg(const ConvArgs* lv, int n, hipStream_t st) {
+  if (n != 3) {
+    set_error("conv_r3 group: %d levels (3 expected)", n);
+    return SFA_E_UNSUPPORTED;
+  }
+  int ord[3] = {0, 1, 2};
+  for (int i = 1; i < 3; ++i)
+    for (int j = i; j > 0 && lv[ord[j]].Kpad > lv[ord[j - 1]].Kpad; --j) std::swap(ord[j], ord[j - 1]);
+  long long start[4] = {0, 0, 0, 0};
+  for (int i = 0; i < 3; ++i) {
+    const ConvArgs& a = lv[ord[i]];
+    const int crc = conv_r3_check<BM, BN, EPI_HEAD, ABL>(a);
+    if (crc != SFA_OK) return crc;
+    if (a.nseg != 1 || a.ksplit > 1) {
+      set_error("conv_r3 group: level %d is not a one-segment, unsplit conv", ord[i]);
+      return SFA_E_UNSUPPORTED;
+    }
+    const long long tiles = (long long)ceil_div(a.M, BM) * (a.N / BN);
+    start[i + 1] = start[i] + (tiles + 7) / 8 * 8;
+  }
+  if (start[3] <= 0 || start[3] > 0x7fffffffll) {
+    set_error("conv_r3 group: bad grid");
+    return SFA_E_INVALID;
+  }
+  hipLaunchKernelGGL((conv_r3_group_kernel<BM, BN, WM, OCC, NSTAGE, ABL>), dim3((unsigned)start[3]),
+                     dim3((BM / WM) * 64), 0, st, lv[ord[0]], lv[ord[1]], lv[ord[2]], (int)start[1], (int)start[2]);
+  SFA_LAUNCH_CHECK();
   return SFA_OK;
 }
 

@@ -715,31 +715,54 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
   }
   const int grid = ntiles < ncu ? ntiles : ncu;
   if (grid <= 0) return SFA_OK;
+  const int abl = a.stem_abl;  // SFA_OPT_STEM_ABL of the model (timing ablations only)
   const dim3 gd((unsigned)grid), bd(stem_patch::NT);
-  // the one-barrier kernel with waves 4-7 issuing their MFMAs first (it reads NCHW3 planes as
-  // aligned float4 column groups); an NCHW3 input that is not 16-B aligned takes the round-3a
-  // three-barrier kernel (4-B plane reads). The timing ablations and the rejected variants live in
-  // tools/experiments/r03/stem_patch_kernel.h.
-  const bool al16 = (reinterpret_cast<uintptr_t>(a.seg[0].x) & 15) == 0;
-  if (!a.part) {
-    set_error("stem_patch: the pooled tile-border parts need the side buffer (a.part)");
-    return SFA_E_INVALID;
+  constexpr int NC3 = STEM_IN_NCHW3;  // ablations: the bench's input layout
+  if (abl != 0 && a.stem_in != NC3) {
+    set_error("stem_patch: ablations are built for the NCHW3 input only");
+    return SFA_E_UNSUPPORTED;
   }
-  if (al16 || a.stem_in == STEM_IN_NHWC4) {
-    switch (a.stem_in) {
-      case STEM_IN_NCHW3: hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3, 1>), gd, bd, 0, st, a, ntiles); break;
-      case STEM_IN_NCHW3_FLIP:
-        hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3_FLIP, 1>), gd, bd, 0, st, a, ntiles);
+  switch (abl) {
+    case 1: hipLaunchKernelGGL((stem_patch_pool_kernel<1, NC3>), gd, bd, 0, st, a, ntiles); break;
+    case 2: hipLaunchKernelGGL((stem_patch_pool_kernel<2, NC3>), gd, bd, 0, st, a, ntiles); break;
+    case 4: hipLaunchKernelGGL((stem_patch_pool_kernel<4, NC3>), gd, bd, 0, st, a, ntiles); break;
+    case 3: hipLaunchKernelGGL((stem_patch_pool_kernel<3, NC3>), gd, bd, 0, st, a, ntiles); break;
+    case 8: hipLaunchKernelGGL((stem_patch_pool_kernel<8, NC3>), gd, bd, 0, st, a, ntiles); break;
+    case 16: hipLaunchKernelGGL((stem_patch_pool_kernel<16, NC3>), gd, bd, 0, st, a, ntiles); break;
+    case 64: hipLaunchKernelGGL((stem_patch_pool_kernel<64, NC3>), gd, bd, 0, st, a, ntiles); break;
+    default:
+      // default: the one-barrier kernel with waves 4-7 issuing their MFMAs first (it reads NCHW3
+      // planes as aligned float4 column groups); tune bit 262144: one barrier, all waves in the
+      // same order; bit 524288: the three-barrier kernel (round 3a)
+      const bool al16 = (reinterpret_cast<uintptr_t>(a.seg[0].x) & 15) == 0;
+      if (a.part && !(a.tune & 524288) && (al16 || a.stem_in == STEM_IN_NHWC4)) {
+        const bool same = (a.tune & 262144) != 0;
+        switch (a.stem_in) {
+          case STEM_IN_NCHW3:
+            if (same) hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3, 0>), gd, bd, 0, st, a, ntiles);
+            else hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3, 1>), gd, bd, 0, st, a, ntiles);
+            break;
+          case STEM_IN_NCHW3_FLIP:
+            if (same) hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3_FLIP, 0>), gd, bd, 0, st, a, ntiles);
+            else hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3_FLIP, 1>), gd, bd, 0, st, a, ntiles);
+            break;
+          default:
+            if (same) hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NHWC4, 0>), gd, bd, 0, st, a, ntiles);
+            else hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NHWC4, 1>), gd, bd, 0, st, a, ntiles);
+            break;
+        }
         break;
-      default: hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NHWC4, 1>), gd, bd, 0, st, a, ntiles); break;
-    }
-  } else if (a.stem_in == STEM_IN_NCHW3) {
-    hipLaunchKernelGGL((stem_patch_pool_kernel<0, STEM_IN_NCHW3>), gd, bd, 0, st, a, ntiles);
-  } else {
-    hipLaunchKernelGGL((stem_patch_pool_kernel<0, STEM_IN_NCHW3_FLIP>), gd, bd, 0, st, a, ntiles);
+      }
+      switch (a.stem_in) {
+        case STEM_IN_NCHW3: hipLaunchKernelGGL((stem_patch_pool_kernel<0, STEM_IN_NCHW3>), gd, bd, 0, st, a, ntiles); break;
+        case STEM_IN_NCHW3_FLIP:
+          hipLaunchKernelGGL((stem_patch_pool_kernel<0, STEM_IN_NCHW3_FLIP>), gd, bd, 0, st, a, ntiles);
+          break;
+        default: hipLaunchKernelGGL((stem_patch_pool_kernel<0, STEM_IN_NHWC4>), gd, bd, 0, st, a, ntiles); break;
+      }
   }
   SFA_LAUNCH_CHECK();
-  {
+  if (a.part) {
     const long long n = (long long)ntiles * 15 * 16;
     hipLaunchKernelGGL(stem_pool_merge_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, a, frames);
   }
