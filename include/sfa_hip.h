@@ -233,6 +233,35 @@ int sfa_decode(const float* hm, const float* off, const float* dir, const float*
                int apply_sigmoid, float* dets, void* workspace, size_t workspace_bytes,
                void* stream);
 
+/* The reference's decode helpers, each on its own (utils/evaluation_utils.py; the drop-in
+ * utils.evaluation_utils serves them from these, so no caller falls through to torch code):
+ *
+ * sfa_heat_nms replaces :21-26 _nms(heat, kernel=3): out = heat * (max_pool2d(heat, 3, 1, 1) ==
+ * heat) over `maps` float32 maps of height x width (pool padded with -inf; non-peaks become the
+ * signed zero of the multiply).  out must not alias heat.
+ *
+ * sfa_topk replaces :47-62 _topk(scores, K) (per_channel = 0) and :65-74 _topk_channel
+ * (per_channel = 1) on float32 (B, C, H, W) scores (no peak test; decode's sfa_decode fuses it):
+ *   per_channel = 0: out_scores f32 (B, K), out_inds int64 (B, K) (flat index within the class
+ *     map), out_clses int32 (B, K), out_ys / out_xs f32 (B, K) = floor(ind / W), ind % W;
+ *   per_channel = 1: out_scores, out_inds, out_ys, out_xs of shape (B, C, K); out_clses unused.
+ * Each class's K by (value desc, index asc), then the classes' C*K by (value desc, class asc,
+ * rank asc) — torch.topk's two stages, its unspecified tie order made definite.  Constraints as
+ * sfa_decode (K <= 256, K <= H*W <= 36864, C <= 16); workspace sfa_topk_workspace_size(B, C, K).
+ *
+ * sfa_gather_feat replaces :29-37 _gather_feat(feat, ind) (mask None: stride_n = dim, stride_d = 1,
+ * feat (B, n, dim)) and :40-44 _transpose_and_gather_feat (feat (B, dim, H, W): n = H*W,
+ * stride_n = 1, stride_d = H*W): out[b][k][d] = feat[b*n*dim + ind[b][k]*stride_n + d*stride_d],
+ * elements of elem_bytes 4 (f32 / int32) or 8 (int64); ind int64 (B, K) in [0, n), checked by the
+ * caller (torch.gather's contract). */
+int sfa_heat_nms(const float* heat, float* out, int64_t maps, int height, int width, void* stream);
+size_t sfa_topk_workspace_size(int batch, int num_classes, int K);
+int sfa_topk(const float* scores, int batch, int num_classes, int height, int width, int K, int per_channel,
+             float* out_scores, int64_t* out_inds, int32_t* out_clses, float* out_ys, float* out_xs,
+             void* workspace, size_t workspace_bytes, void* stream);
+int sfa_gather_feat(const void* feat, int batch, int64_t n, int dim, int64_t stride_n, int64_t stride_d,
+                    int elem_bytes, const int64_t* ind, int K, void* out, void* stream);
+
 /* ------------------------------------------------ post-processing on device --
  * the SFA side of the fusion scripts without a host hop.
  *

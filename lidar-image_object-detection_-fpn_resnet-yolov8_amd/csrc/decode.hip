@@ -78,6 +78,8 @@ __device__ int block_excl_scan(int v, int* wsum /*[16]*/, int* total) {
   return before + x - v;
 }
 
+// PEAK = false: no 3x3 peak test (the reference's _topk / _topk_channel on a map as it is).
+template <bool PEAK = true>
 __global__ void __launch_bounds__(kDecThreads) decode_class_topk_kernel(
     const float* __restrict__ hm, int C, int H, int W, int K, int apply_sigmoid,
     unsigned* __restrict__ cand_key, int* __restrict__ cand_idx) {
@@ -123,13 +125,15 @@ __global__ void __launch_bounds__(kDecThreads) decode_class_topk_kernel(
     if (i < i1) {
       const float v = heat[i];
       float m = v;
-      for (int dy = -1; dy <= 1; ++dy) {
-        const int yy = y + dy;
-        if ((unsigned)yy >= (unsigned)H) continue;
-        for (int dx = -1; dx <= 1; ++dx) {
-          const int xx = x + dx;
-          if ((unsigned)xx >= (unsigned)W) continue;
-          m = fmaxf(m, heat[yy * W + xx]);
+      if (PEAK) {
+        for (int dy = -1; dy <= 1; ++dy) {
+          const int yy = y + dy;
+          if ((unsigned)yy >= (unsigned)H) continue;
+          for (int dx = -1; dx <= 1; ++dx) {
+            const int xx = x + dx;
+            if ((unsigned)xx >= (unsigned)W) continue;
+            m = fmaxf(m, heat[yy * W + xx]);
+          }
         }
       }
       out = (m == v) ? v : v * 0.f;  // heat * keep: non-peaks become (signed) zero
@@ -319,7 +323,7 @@ __device__ int band_excl_scan(int v, int* wsum /*[kBandWaves]*/) {
 // the map and columns -1 / W), so the 3x3 peak test is nine unconditional reads.  Writes the
 // band's top min(K, band pixels) by (value desc, index asc) as a sorted list of K (key, index),
 // padded with sentinels (key 0, index INT_MAX), to bkey / bidx[((b * C + c) * S + s) * K + j].
-template <int ABL = 0>
+template <int ABL = 0, bool PEAK = true>
 __global__ void __launch_bounds__(kBandThreads) decode_band_topk_kernel(
     const float* __restrict__ hm, int C, int H, int W, int K, int R, int apply_sigmoid,
     unsigned* __restrict__ bkey, int* __restrict__ bidx) {
@@ -371,7 +375,7 @@ __global__ void __launch_bounds__(kBandThreads) decode_band_topk_kernel(
         const float* t = tile + (r + 1) * TW + x + 1;  // the pixel; neighbours at +-1, +-TW
         const float v = t[0];
         float m = v;
-        if (!(ABL & 2)) {
+        if (PEAK && !(ABL & 2)) {
           const float a0 = fmaxf(fmaxf(t[-TW - 1], t[-TW]), t[-TW + 1]);
           const float a1 = fmaxf(t[-1], t[1]);
           const float a2 = fmaxf(fmaxf(t[TW - 1], t[TW]), t[TW + 1]);
@@ -614,6 +618,154 @@ static void band_plan(int C, int H, int W, int K, int* S_out, int* R_out) {
   }
 }
 
+// ---------------------------------------------------------------- helpers --
+// The reference's decode helpers as device functions of their own (the drop-in
+// utils.evaluation_utils serves them; VERDICT r03: no hot-path name may fall through to the
+// reference's torch code).
+
+// _nms (evaluation_utils.py:21-26): out = heat * (max_pool2d(heat, 3, 1, 1) == heat), the pool
+// padded with -inf (neighbours outside the map are skipped), non-peaks (signed) zero like the
+// float multiply. One thread per pixel; the nine reads hit L1 / L2 (out must not alias heat).
+__global__ void __launch_bounds__(256) heat_nms_kernel(const float* __restrict__ heat, float* __restrict__ out,
+                                                       int64_t n, int H, int W) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t HW = (int64_t)H * W;
+  const int64_t p = i % HW;
+  const int y = (int)(p / W), x = (int)(p - (int64_t)(p / W) * W);
+  const float* map = heat + (i - p);
+  const float v = heat[i];
+  float m = v;
+  for (int dy = -1; dy <= 1; ++dy) {
+    const int yy = y + dy;
+    if ((unsigned)yy >= (unsigned)H) continue;
+    for (int dx = -1; dx <= 1; ++dx) {
+      const int xx = x + dx;
+      if ((unsigned)xx >= (unsigned)W) continue;
+      m = fmaxf(m, map[(int64_t)yy * W + xx]);
+    }
+  }
+  out[i] = (m == v) ? v : v * 0.f;
+}
+
+// _topk (:47-62, PERCH = false) / _topk_channel (:65-74, PERCH = true) outputs from the band
+// lists of decode_band_topk_kernel<0, false> (no peak test). One workgroup per output group: a
+// frame (its C * S lists, merged in (value desc, class asc, index asc) order = torch's second
+// topk over class * K + rank), or a (frame, class) (its S lists: the class's own top K).  Columns
+// as the reference computes them: score, ind (the flat index within the class map, int64),
+// class (int32, PERCH = false), ys = floor(ind / W), xs = ind % W (floats).
+template <bool PERCH>
+__global__ void __launch_bounds__(1024) topk_band_merge_kernel(
+    const unsigned* __restrict__ bkey, const int* __restrict__ bidx, int C, int S, int K, int W,
+    float* __restrict__ out_score, int64_t* __restrict__ out_inds, int* __restrict__ out_cls,
+    float* __restrict__ out_ys, float* __restrict__ out_xs) {
+  __shared__ unsigned skey[2][kMergeMax];
+  __shared__ int sidx[2][kMergeMax];  // class * 2^26 + index
+  const int g = blockIdx.x;
+  const int SK = S * K, N = PERCH ? SK : C * SK;
+  for (int t = threadIdx.x; t < N; t += blockDim.x) {
+    const unsigned k = bkey[(size_t)g * N + t];
+    const int ix = bidx[(size_t)g * N + t];
+    skey[0][t] = k;
+    sidx[0][t] = ix == 0x7fffffff ? 0x7fffffff : (t / SK) * (1 << 26) + ix;
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int nl = N / K; nl > 1; nl = (nl + 1) >> 1) {
+    const unsigned* ik = skey[cur];
+    const int* ii = sidx[cur];
+    unsigned* ok = skey[cur ^ 1];
+    int* oi = sidx[cur ^ 1];
+    for (int t = threadIdx.x; t < nl * K; t += blockDim.x) {
+      const int l = t / K, p = t - l * K;
+      const unsigned k = ik[t];
+      const int ci = ii[t];
+      int rank = p;
+      if (!((nl & 1) && l == nl - 1)) {
+        const bool left = (l & 1) == 0;
+        const unsigned* pk = ik + (l ^ 1) * K;
+        const int* pi = ii + (l ^ 1) * K;
+        int lo = 0, hi = K;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          const unsigned km = pk[mid];
+          const int im = pi[mid];
+          const bool before = km > k || (km == k && (left ? im < ci : im <= ci));
+          if (before)
+            lo = mid + 1;
+          else
+            hi = mid;
+        }
+        rank += lo;
+      }
+      if (rank < K) {
+        ok[(l >> 1) * K + rank] = k;
+        oi[(l >> 1) * K + rank] = ci;
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  for (int rank = threadIdx.x; rank < K; rank += blockDim.x) {
+    const unsigned k = skey[cur][rank];
+    const int ci = sidx[cur][rank];
+    const int ind = ci & ((1 << 26) - 1);
+    const size_t o = (size_t)g * K + rank;
+    out_score[o] = fkey_inv(k);
+    out_inds[o] = ind;
+    if (!PERCH) out_cls[o] = ci >> 26;
+    out_ys[o] = (float)(ind / W);
+    out_xs[o] = (float)(ind % W);
+  }
+}
+
+// The same outputs from the one-block-per-class candidates (decode_class_topk_kernel<false>:
+// each class's K sorted by (value desc, index asc)) for maps whose bands do not fit LDS.
+template <bool PERCH>
+__global__ void __launch_bounds__(256) topk_class_out_kernel(
+    const unsigned* __restrict__ cand_key, const int* __restrict__ cand_idx, int C, int K, int W,
+    float* __restrict__ out_score, int64_t* __restrict__ out_inds, int* __restrict__ out_cls,
+    float* __restrict__ out_ys, float* __restrict__ out_xs) {
+  const int g = blockIdx.x;
+  const int N = PERCH ? K : C * K;
+  const unsigned* ck = cand_key + (size_t)g * N;
+  const int* ci = cand_idx + (size_t)g * N;
+  for (int t = threadIdx.x; t < N; t += blockDim.x) {
+    const unsigned k = ck[t];
+    int rank = t;
+    if (!PERCH) {  // torch's second topk: value desc, then class * K + rank asc
+      rank = 0;
+      for (int j = 0; j < N; ++j) {
+        const unsigned kj = ck[j];
+        rank += (kj > k) || (kj == k && j < t);
+      }
+      if (rank >= K) continue;
+    }
+    const int ind = ci[t];
+    const size_t o = (size_t)g * K + rank;
+    out_score[o] = fkey_inv(k);
+    out_inds[o] = ind;
+    if (!PERCH) out_cls[o] = t / K;
+    out_ys[o] = (float)(ind / W);
+    out_xs[o] = (float)(ind % W);
+  }
+}
+
+// _gather_feat (:29-37, mask None) and _transpose_and_gather_feat (:40-44): out[b][k][d] =
+// feat[b * N * D + ind[b][k] * stride_n + d * stride_d] (elements of elem_bytes = 4 or 8:
+// f32 / int32 features, or the int64 indices _topk gathers); indices checked by the caller.
+template <typename T>
+__global__ void __launch_bounds__(256) gather_feat_kernel(const T* __restrict__ feat, int64_t N, int D,
+                                                          int64_t sn, int64_t sd, const int64_t* __restrict__ ind,
+                                                          int K, int64_t total, T* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int d = (int)(i % D);
+  const int64_t bk = i / D;
+  const int64_t b = bk / K;
+  out[i] = feat[b * N * D + ind[bk] * sn + (int64_t)d * sd];
+}
+
 }  // namespace sfa
 
 using namespace sfa;
@@ -661,10 +813,94 @@ extern "C" int sfa_decode(const float* hm, const float* off, const float* dir, c
   auto* ck = reinterpret_cast<unsigned*>(workspace);
   auto* ci = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) +
                                     align_up(n * sizeof(unsigned), 256));
-  hipLaunchKernelGGL(decode_class_topk_kernel, dim3(batch * num_classes), dim3(kDecThreads), 0, st, hm, num_classes, height, width, K, apply_sigmoid, ck, ci);
+  hipLaunchKernelGGL(decode_class_topk_kernel<true>, dim3(batch * num_classes), dim3(kDecThreads), 0, st, hm, num_classes, height, width, K, apply_sigmoid, ck, ci);
   SFA_LAUNCH_CHECK();
   hipLaunchKernelGGL(decode_merge_gather_kernel, dim3(batch), dim3(256), 0, st, ck, ci,
                      num_classes, K, height, width, apply_sigmoid, off, dir, z, dim, dets);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+extern "C" int sfa_heat_nms(const float* heat, float* out, int64_t maps, int height, int width, void* stream) {
+  SFA_CHECK_ARG(maps >= 0 && height >= 1 && width >= 1, "heat_nms: bad shape");
+  const int64_t n = maps * (int64_t)height * width;
+  if (n == 0) return SFA_OK;
+  SFA_CHECK_ARG(heat && out && heat != out, "heat_nms: null or aliased buffers");
+  hipLaunchKernelGGL(heat_nms_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), heat, out, n, height, width);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+extern "C" size_t sfa_topk_workspace_size(int batch, int num_classes, int K) {
+  return sfa_decode_workspace_size(batch, num_classes, K);
+}
+
+extern "C" int sfa_topk(const float* scores, int batch, int num_classes, int height, int width, int K,
+                        int per_channel, float* out_scores, int64_t* out_inds, int32_t* out_clses, float* out_ys,
+                        float* out_xs, void* workspace, size_t workspace_bytes, void* stream) {
+  SFA_CHECK_ARG(scores && out_scores && out_inds && out_ys && out_xs && workspace && (per_channel || out_clses),
+                "topk: null argument");
+  SFA_CHECK_ARG(batch >= 1 && num_classes >= 1 && num_classes <= 16, "topk: bad B/C");
+  SFA_CHECK_ARG(height >= 1 && width >= 1 && height * width <= kDecMaxHW, "topk: H*W = %d exceeds %d",
+                height * width, kDecMaxHW);
+  SFA_CHECK_ARG(K >= 1 && K <= kDecMaxK && K <= height * width, "topk: K = %d out of range", K);
+  if (workspace_bytes < sfa_topk_workspace_size(batch, num_classes, K)) {
+    set_error("topk: workspace too small");
+    return SFA_E_WORKSPACE;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int groups = per_channel ? batch * num_classes : batch;
+  int S = 0, R = height;
+  band_plan(num_classes, height, width, K, &S, &R);
+  if (S > 0) {
+    const size_t nb = (size_t)batch * num_classes * S * K;
+    auto* bk = reinterpret_cast<unsigned*>(workspace);
+    auto* bi = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + align_up(nb * sizeof(unsigned), 256));
+    hipLaunchKernelGGL((decode_band_topk_kernel<0, false>), dim3(S, num_classes, batch), dim3(kBandThreads), 0, st,
+                       scores, num_classes, height, width, K, R, 0, bk, bi);
+    SFA_LAUNCH_CHECK();
+    if (per_channel)
+      hipLaunchKernelGGL(topk_band_merge_kernel<true>, dim3(groups), dim3(1024), 0, st, bk, bi, num_classes, S, K,
+                         width, out_scores, out_inds, out_clses, out_ys, out_xs);
+    else
+      hipLaunchKernelGGL(topk_band_merge_kernel<false>, dim3(groups), dim3(1024), 0, st, bk, bi, num_classes, S, K,
+                         width, out_scores, out_inds, out_clses, out_ys, out_xs);
+    SFA_LAUNCH_CHECK();
+    return SFA_OK;
+  }
+  const size_t n = (size_t)batch * num_classes * K;
+  auto* ck = reinterpret_cast<unsigned*>(workspace);
+  auto* ci = reinterpret_cast<int*>(reinterpret_cast<char*>(workspace) + align_up(n * sizeof(unsigned), 256));
+  hipLaunchKernelGGL(decode_class_topk_kernel<false>, dim3(batch * num_classes), dim3(kDecThreads), 0, st, scores,
+                     num_classes, height, width, K, 0, ck, ci);
+  SFA_LAUNCH_CHECK();
+  if (per_channel)
+    hipLaunchKernelGGL(topk_class_out_kernel<true>, dim3(groups), dim3(256), 0, st, ck, ci, num_classes, K, width,
+                       out_scores, out_inds, out_clses, out_ys, out_xs);
+  else
+    hipLaunchKernelGGL(topk_class_out_kernel<false>, dim3(groups), dim3(256), 0, st, ck, ci, num_classes, K, width,
+                       out_scores, out_inds, out_clses, out_ys, out_xs);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+extern "C" int sfa_gather_feat(const void* feat, int batch, int64_t n, int dim, int64_t stride_n, int64_t stride_d,
+                               int elem_bytes, const int64_t* ind, int K, void* out, void* stream) {
+  SFA_CHECK_ARG(batch >= 0 && n >= 1 && dim >= 1 && K >= 0 && (elem_bytes == 4 || elem_bytes == 8),
+                "gather_feat: bad shape");
+  const int64_t total = (int64_t)batch * K * dim;
+  if (total == 0) return SFA_OK;
+  SFA_CHECK_ARG(feat && ind && out, "gather_feat: null argument");
+  const dim3 g((unsigned)((total + 255) / 256)), b(256);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (elem_bytes == 4)
+    hipLaunchKernelGGL(gather_feat_kernel<unsigned>, g, b, 0, st, reinterpret_cast<const unsigned*>(feat), n, dim,
+                       stride_n, stride_d, ind, K, total, reinterpret_cast<unsigned*>(out));
+  else
+    hipLaunchKernelGGL(gather_feat_kernel<unsigned long long>, g, b, 0, st,
+                       reinterpret_cast<const unsigned long long*>(feat), n, dim, stride_n, stride_d, ind, K, total,
+                       reinterpret_cast<unsigned long long*>(out));
   SFA_LAUNCH_CHECK();
   return SFA_OK;
 }

@@ -22,17 +22,9 @@ from sfa_hip import _lib, runtime
 from sfa_hip import dropin as _dropin
 
 
-def _device(device=None):
-    if device is not None:
-        return torch.device(device)
-    if not torch.cuda.is_available():
-        raise _lib.SfaNativeError("makeBEVMap runs on the GPU (HIP); no GPU is visible")
-    return torch.device("cuda", torch.cuda.current_device())
-
-
 def makeBEVMap(PointCloud_, boundary, device=None):
     """Reference-compatible host API (float64 result)."""
-    dev = _device(device)
+    dev = runtime.host_api_device("makeBEVMap", device)
     pts = np.ascontiguousarray(PointCloud_, dtype=np.float32)
     if pts.ndim != 2 or pts.shape[1] != 4:
         raise ValueError(f"PointCloud_ must be (N, 4), got {pts.shape}")

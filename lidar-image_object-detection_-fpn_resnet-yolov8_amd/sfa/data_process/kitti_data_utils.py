@@ -26,19 +26,23 @@ def get_filtered_lidar(lidar, boundary, labels=None):
     if isinstance(lidar, torch.Tensor):
         out = runtime.filter_points(lidar, boundary)
     else:
-        if not torch.cuda.is_available():
-            raise runtime.SfaNativeError("get_filtered_lidar runs on the GPU (HIP); no GPU visible")
         pts = np.ascontiguousarray(lidar, dtype=np.float32)
-        dev = torch.device("cuda", torch.cuda.current_device())
+        dev = runtime.host_api_device("get_filtered_lidar")
         out = runtime.filter_points(torch.from_numpy(pts).to(dev), boundary).cpu().numpy()
     if labels is None:
         return out
+    return out, filter_labels(labels, boundary)
+
+
+def filter_labels(labels, boundary):
+    """The label half of get_filtered_lidar (:244-249): half-open box test on the label rows'
+    x, y, z (host numpy, as the reference)."""
     minX, maxX = boundary["minX"], boundary["maxX"]
     minY, maxY = boundary["minY"], boundary["maxY"]
     minZ, maxZ = boundary["minZ"], boundary["maxZ"]
     keep = ((labels[:, 1] >= minX) & (labels[:, 1] < maxX) & (labels[:, 2] >= minY) &
             (labels[:, 2] < maxY) & (labels[:, 3] >= minZ) & (labels[:, 3] < maxZ))
-    return out, labels[keep]
+    return labels[keep]
 
 
 class Calibration(object):

@@ -26,6 +26,22 @@ from sfa_hip.runtime import KfpnEngine, pack_state_dict
 
 BN_MOMENTUM = 0.1
 
+# Generation of the module structure of the process: bumped whenever any module registers a
+# parameter, buffer or submodule (torch's global registration hooks) and when PoseResNet._apply
+# swaps tensors, so PoseResNet can keep its list of state tensors between forwards and re-walk
+# state_dict() only when the structure may have changed (a state_dict walk is ~1.1 ms of host
+# time per forward, the cached list's (data_ptr, _version) check ~40 us).
+_STRUCT_GEN = [0]
+
+
+def _bump_struct_gen(*_args, **_kw):
+    _STRUCT_GEN[0] += 1
+
+
+torch.nn.modules.module.register_module_parameter_registration_hook(_bump_struct_gen)
+torch.nn.modules.module.register_module_buffer_registration_hook(_bump_struct_gen)
+torch.nn.modules.module.register_module_module_registration_hook(_bump_struct_gen)
+
 model_urls = {
     "resnet18": "https://download.pytorch.org/models/resnet18-5c106cde.pth",
 }
@@ -91,6 +107,7 @@ class PoseResNet(nn.Module):
         self._arch = _lib.make_arch(dict(self.heads), head_conv)
         self._engines = {}
         self._sig = None
+        self._state_tensors = None  # (structure generation, [state tensors]) cache of _signature
 
     def _make_layer(self, block, planes, blocks, stride=1):
         downsample = None
@@ -105,7 +122,17 @@ class PoseResNet(nn.Module):
 
     # -------------------------------------------------------------- engine
     def _signature(self):
-        return tuple((t.data_ptr(), t._version) for t in self.state_dict(keep_vars=True).values())
+        """(data_ptr, version) of every state tensor: any in-place update, reload or move of a
+        parameter changes it, and the engine repacks the weights."""
+        cache = self._state_tensors
+        if cache is None or cache[0] != _STRUCT_GEN[0]:
+            cache = self._state_tensors = (_STRUCT_GEN[0], list(self.state_dict(keep_vars=True).values()))
+        return tuple((t.data_ptr(), t._version) for t in cache[1])
+
+    def _apply(self, fn, *args, **kw):  # .to() / .cuda() / .float() may replace the tensors
+        out = super()._apply(fn, *args, **kw)
+        _bump_struct_gen()
+        return out
 
     def _engine(self, device) -> KfpnEngine:
         sig = self._signature()

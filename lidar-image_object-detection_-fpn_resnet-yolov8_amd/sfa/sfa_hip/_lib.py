@@ -85,6 +85,11 @@ PROBE_HEADS, PROBE_SERIAL = 1, 2
 _PROTOS["sfa_model_set_probe"] = (_c_int, [_vp, _c_int])
 _PROTOS["sfa_model_set_side_streams"] = (_c_int, [_vp, _c_int])
 _PROTOS["sfa_model_probe_times"] = (_c_int, [_vp, ctypes.POINTER(ctypes.c_float), _c_int])
+_PROTOS["sfa_heat_nms"] = (_c_int, [_vp, _vp, _c_i64, _c_int, _c_int, _vp])
+_PROTOS["sfa_topk_workspace_size"] = (_c_size, [_c_int, _c_int, _c_int])
+_PROTOS["sfa_topk"] = (_c_int, [_vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp,
+                                _vp, _c_size, _vp])
+_PROTOS["sfa_gather_feat"] = (_c_int, [_vp, _c_int, _c_i64, _c_int, _c_i64, _c_i64, _c_int, _vp, _c_int, _vp, _vp])
 
 
 def math_from_env(default=MATH_FP16X3) -> int:

@@ -30,6 +30,25 @@ def _require_gpu_tensor(t: torch.Tensor, what: str, dtype=torch.float32) -> torc
     return t.contiguous()
 
 
+def host_api_device(what: str, device=None) -> torch.device:
+    """The GPU a numpy-in / numpy-out host API (makeBEVMap, get_filtered_lidar) runs on: ``device``
+    or the current one. Raises SfaNativeError with the fix when no GPU is visible or when called in a
+    process forked after HIP was initialised — a DataLoader worker of a caller that created its model
+    first (test.py:112 then :120): HIP cannot be used there, and the drop-in's
+    data_process.kitti_dataloader voxelises each batch in the main process instead."""
+    if device is not None:
+        return torch.device(device)
+    if torch.cuda._is_in_bad_fork():
+        raise SfaNativeError(
+            f"{what} runs on the GPU (HIP), but this process was forked after HIP was initialised "
+            "(a DataLoader worker): create the loader with the drop-in data_process.kitti_dataloader "
+            "(create_test_dataloader / create_val_dataloader / create_train_dataloader: the workers only "
+            "read files, the BEV maps are made per batch in the main process) or use num_workers=0")
+    if not torch.cuda.is_available():
+        raise SfaNativeError(f"{what} runs on the GPU (HIP); no GPU is visible")
+    return torch.device("cuda", torch.cuda.current_device())
+
+
 def _boundary_arr(boundary: dict):
     vals = [boundary[k] for k in ("minX", "maxX", "minY", "maxY", "minZ", "maxZ")]
     return (ctypes.c_double * 6)(*[float(v) for v in vals])
@@ -321,11 +340,90 @@ def filter_points(points: torch.Tensor, boundary=DEFAULT_BOUNDARY) -> torch.Tens
 
 # ------------------------------------------------------------------ decode
 def sigmoid_clamp_(x: torch.Tensor) -> torch.Tensor:
-    if x.device.type != "cuda" or not x.is_contiguous() or x.dtype != torch.float32:
-        raise SfaNativeError("_sigmoid: the HIP path needs a contiguous float32 GPU tensor")
-    check(lib().sfa_sigmoid_clamp_inplace(x.data_ptr(), x.numel(), _lib.stream_ptr(x.device)),
+    """_sigmoid (utils/torch_utils.py:44-45) in place on a float32 GPU tensor; a non-contiguous
+    one (the reference accepts any strided tensor) goes through a contiguous copy that is
+    written back into it."""
+    if not isinstance(x, torch.Tensor) or x.device.type != "cuda" or x.dtype != torch.float32:
+        raise SfaNativeError("_sigmoid: the HIP path needs a float32 GPU tensor")
+    if x.numel() == 0:
+        return x
+    t = x if x.is_contiguous() else x.contiguous()
+    check(lib().sfa_sigmoid_clamp_inplace(t.data_ptr(), t.numel(), _lib.stream_ptr(x.device)),
           "sfa_sigmoid_clamp_inplace")
+    if t is not x:
+        x.copy_(t)
     return x
+
+
+def heat_nms(heat: torch.Tensor) -> torch.Tensor:
+    """_nms (evaluation_utils.py:21-26, kernel 3): a new tensor heat * (max_pool3x3(heat) == heat)."""
+    heat = _require_gpu_tensor(heat, "_nms")
+    if heat.dim() < 2:
+        raise ValueError("_nms: expected (..., H, W)")
+    H, W = int(heat.shape[-2]), int(heat.shape[-1])
+    out = torch.empty_like(heat)
+    check(lib().sfa_heat_nms(heat.data_ptr() if heat.numel() else None, out.data_ptr() if out.numel() else None,
+                             heat.numel() // max(1, H * W), H, W, _lib.stream_ptr(heat.device)), "sfa_heat_nms")
+    return out
+
+
+def topk(scores: torch.Tensor, K: int = 40, per_channel: bool = False):
+    """_topk (evaluation_utils.py:47-62): (score (B,K) f32, inds (B,K) int64, clses (B,K) int32,
+    ys (B,K) f32, xs (B,K) f32); per_channel = _topk_channel (:65-74): (scores, inds, ys, xs), each
+    (B, C, K). Ties: lower flat index first, then lower class (torch leaves them unspecified)."""
+    scores = _require_gpu_tensor(scores, "_topk")
+    if scores.dim() != 4:
+        raise ValueError(f"_topk: expected (B, C, H, W), got {tuple(scores.shape)}")
+    B, C, H, W = (int(v) for v in scores.shape)
+    K = int(K)
+    if K > H * W:  # torch.topk: "selected index k out of range"
+        raise RuntimeError(f"_topk: K = {K} exceeds the {H * W} elements of a class map")
+    dev = scores.device
+    shp = (B, C, K) if per_channel else (B, K)
+    sc = torch.empty(shp, dtype=torch.float32, device=dev)
+    ind = torch.empty(shp, dtype=torch.int64, device=dev)
+    cls = None if per_channel else torch.empty(shp, dtype=torch.int32, device=dev)
+    ys = torch.empty(shp, dtype=torch.float32, device=dev)
+    xs = torch.empty(shp, dtype=torch.float32, device=dev)
+    ws = torch.empty(int(lib().sfa_topk_workspace_size(B, C, K)), dtype=torch.uint8, device=dev)
+    check(lib().sfa_topk(scores.data_ptr(), B, C, H, W, K, 1 if per_channel else 0, sc.data_ptr(), ind.data_ptr(),
+                         cls.data_ptr() if cls is not None else None, ys.data_ptr(), xs.data_ptr(), ws.data_ptr(),
+                         ws.numel(), _lib.stream_ptr(dev)), "sfa_topk")
+    return (sc, ind, ys, xs) if per_channel else (sc, ind, cls, ys, xs)
+
+
+def gather_feat(feat: torch.Tensor, ind: torch.Tensor, transpose: bool = False) -> torch.Tensor:
+    """_gather_feat (evaluation_utils.py:29-37, mask None): feat (B, N, D), ind (B, K) int64 ->
+    (B, K, D); transpose = _transpose_and_gather_feat (:40-44): feat (B, D, H, W) -> (B, K, D).
+    4- or 8-byte elements (f32, int32, int64). Indices outside [0, N) raise, as torch.gather does."""
+    if not isinstance(feat, torch.Tensor) or feat.device.type != "cuda":
+        raise SfaNativeError("_gather_feat: the HIP path needs GPU tensors; there is no CPU fallback")
+    if feat.element_size() not in (4, 8):
+        raise TypeError(f"_gather_feat: {feat.dtype} elements are not 4 or 8 bytes")
+    ind = _require_gpu_tensor(ind, "_gather_feat indices", torch.int64)
+    feat = feat.contiguous()
+    if transpose:
+        if feat.dim() != 4:
+            raise ValueError("_transpose_and_gather_feat: expected feat (B, C, H, W)")
+        B, D, H, W = (int(v) for v in feat.shape)
+        N, sn, sd = H * W, 1, H * W
+    else:
+        if feat.dim() != 3:
+            raise ValueError("_gather_feat: expected feat (B, N, D)")
+        B, N, D = (int(v) for v in feat.shape)
+        sn, sd = D, 1
+    if ind.dim() != 2 or int(ind.shape[0]) != B:
+        raise ValueError(f"_gather_feat: indices {tuple(ind.shape)} do not match batch {B}")
+    K = int(ind.shape[1])
+    out = torch.empty((B, K, D), dtype=feat.dtype, device=feat.device)
+    if ind.numel():
+        lo, hi = (int(v) for v in torch.aminmax(ind))
+        if lo < 0 or hi >= N:
+            raise RuntimeError(f"_gather_feat: index {lo if lo < 0 else hi} is out of bounds for size {N}")
+    check(lib().sfa_gather_feat(feat.data_ptr() if feat.numel() else None, B, N, D, sn, sd, feat.element_size(),
+                                ind.data_ptr() if ind.numel() else None, K, out.data_ptr() if out.numel() else None,
+                                _lib.stream_ptr(feat.device)), "sfa_gather_feat")
+    return out
 
 
 class Decoder:

@@ -11,6 +11,12 @@
   The reference's per-array prints are emitted only when SFA_VERBOSE=1.
 * ``convert_det_to_real_values`` (:177-193), ``get_yaw`` (:108-109) and
   ``draw_predictions`` (:166-174, needs OpenCV) are host-side like the reference.
+* The decode helpers, for callers that use them on their own: ``_nms`` (:21-26,
+  sfa_heat_nms), ``_topk`` (:47-62) and ``_topk_channel`` (:65-74, sfa_topk),
+  ``_gather_feat`` (:29-37) and ``_transpose_and_gather_feat`` (:40-44, sfa_gather_feat) run on
+  the GPU too (no name of the hot path falls through to the reference's torch code); ties in
+  the top-K ordered as in ``decode``.  ``_gather_feat`` with a ``mask`` (its boolean selection
+  has a data-dependent shape; the reference never passes one) raises NotImplementedError.
 """
 
 from __future__ import annotations
@@ -24,6 +30,30 @@ from sfa_hip import runtime
 from sfa_hip import dropin as _dropin
 
 _VERBOSE = os.environ.get("SFA_VERBOSE", "0") == "1"
+
+
+def _nms(heat, kernel=3):
+    if kernel != 3:
+        raise NotImplementedError(f"_nms: the HIP kernel implements kernel = 3 (got {kernel})")
+    return runtime.heat_nms(heat)
+
+
+def _gather_feat(feat, ind, mask=None):
+    if mask is not None:
+        raise NotImplementedError("_gather_feat with a mask (data-dependent shape) is not on the gfx950 path")
+    return runtime.gather_feat(feat, ind)
+
+
+def _transpose_and_gather_feat(feat, ind):
+    return runtime.gather_feat(feat, ind, transpose=True)
+
+
+def _topk(scores, K=40):
+    return runtime.topk(scores, K)
+
+
+def _topk_channel(scores, K=40):
+    return runtime.topk(scores, K, per_channel=True)
 
 
 def decode(hm_cen, cen_offset, direction, z_coor, dim, K=40):

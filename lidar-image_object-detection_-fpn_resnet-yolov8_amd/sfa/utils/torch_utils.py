@@ -1,8 +1,8 @@
 """Drop-in for the reference's utils/torch_utils.py (hot-path part).
 
 ``_sigmoid`` (:44-45) is in place — sigmoid then clamp(1e-4, 1 - 1e-4) — and
-returns its argument, like the reference; it runs as a HIP kernel
-(sfa_sigmoid_clamp_inplace) and refuses CPU tensors.
+returns its argument, like the reference, for any strided float32 GPU tensor; it runs as a
+HIP kernel (sfa_sigmoid_clamp_inplace) and refuses CPU tensors.
 """
 
 from __future__ import annotations
@@ -16,8 +16,6 @@ from sfa_hip.runtime import sigmoid_clamp_
 
 
 def _sigmoid(x):
-    if not x.is_contiguous():
-        raise ValueError("_sigmoid: in-place HIP kernel needs a contiguous tensor")
     return sigmoid_clamp_(x)
 
 

@@ -196,8 +196,8 @@ sys.path[:0] = [sys.argv[1], sys.argv[2]]; sys.path.append(sys.argv[3])
 out = {}
 for m in ["models.model_utils", "models.fpn_resnet", "utils.evaluation_utils", "utils.torch_utils",
           "data_process.kitti_bev_utils", "data_process.kitti_data_utils", "config.kitti_config",
-          "utils.demo_utils", "data_process.kitti_dataloader", "data_process.transformation",
-          "data_process.demo_dataset", "utils.misc", "utils.visualization_utils"]:
+          "utils.demo_utils", "data_process.kitti_dataloader", "data_process.kitti_dataset",
+          "data_process.transformation", "data_process.demo_dataset", "utils.misc", "utils.visualization_utils"]:
     out[m] = os.path.realpath(importlib.import_module(m).__file__)
 import data_process.kitti_data_utils as kdu
 out["gen_hm_radius"] = kdu.gen_hm_radius.__module__
@@ -218,13 +218,13 @@ print("@@" + json.dumps(out))
     dropin = os.path.realpath(SFA_ROOT)
     for m in ["models.model_utils", "models.fpn_resnet", "utils.evaluation_utils", "utils.torch_utils",
               "data_process.kitti_bev_utils", "data_process.kitti_data_utils", "config.kitti_config",
-              "utils.demo_utils"]:
+              "utils.demo_utils", "data_process.kitti_dataloader", "data_process.kitti_dataset"]:
         assert out[m].startswith(dropin), (m, out[m])
-    for m in ["data_process.kitti_dataloader", "data_process.transformation", "data_process.demo_dataset",
-              "utils.misc", "utils.visualization_utils"]:
+    for m in ["data_process.transformation", "data_process.demo_dataset", "utils.misc", "utils.visualization_utils"]:
         assert out[m].startswith(ref_root), (m, out[m])
     assert out["gen_hm_radius"] == "_sfa_reference.data_process.kitti_data_utils"
-    # the reference's dataset binds the drop-in's (HIP) voxeliser
+    # names the drop-in dataset module does not define come from the reference's module, whose
+    # own imports bind the drop-in's (HIP) voxeliser
     assert out["kitti_dataset.makeBEVMap"] == "data_process.kitti_bev_utils"
     assert out["missing"] == "AttributeError"
 

@@ -140,3 +140,95 @@ def test_decode_band_split_shapes(gpu, B, C, H, W, K):
                          K=K).cpu().numpy()
     exp = decode_oracle.decode(hm, maps["off"], maps["dir"], maps["z"], maps["dim"], K=K)
     np.testing.assert_array_equal(got, exp)
+
+
+# ---- the reference's decode helpers on their own (evaluation_utils.py:21-74): the drop-in serves
+# them from sfa_heat_nms / sfa_topk / sfa_gather_feat, checked against the oracle's restatements
+
+def _scores(B, C, H, W, seed, ties=False):
+    rng = np.random.default_rng(seed)
+    s = rng.permutation(B * C * H * W).astype(np.float32).reshape(B, C, H, W) / (B * C * H * W)  # tie-free
+    if ties:
+        s = np.round(s * 64) / 64  # heavy ties: the order is the documented (index, class) one
+    return s.astype(np.float32)
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 152, 152), (1, 3, 37, 53), (2, 1, 7, 9)])
+def test_nms_helper_bit_exact(gpu, shape):
+    from utils.evaluation_utils import _nms
+    h = _scores(*shape, seed=3, ties=True)  # plateaus: every member of a plateau survives
+    got = _nms(_t(h, gpu))
+    assert got.shape == h.shape and got.device == gpu
+    np.testing.assert_array_equal(got.cpu().numpy(), decode_oracle.nms_peaks(h))
+
+
+@pytest.mark.parametrize("shape,K", [((2, 3, 152, 152), 50), ((3, 3, 64, 64), 40), ((2, 16, 100, 100), 200),
+                                     ((1, 2, 5, 5), 25)])
+@pytest.mark.parametrize("ties", [False, True])
+def test_topk_helpers_match_oracle(gpu, shape, K, ties):
+    """_topk / _topk_channel: the band kernels (152 x 152, 64 x 64) and the one-block-per-class
+    fallback (16 classes x K = 200 over 100 x 100: no band split fits), K = H*W included; with ties the
+    order is lower flat index, then lower class (torch leaves it unspecified)."""
+    from utils.evaluation_utils import _topk, _topk_channel
+    s = _scores(*shape, seed=sum(shape) + K, ties=ties)
+    sc, ind, cls, ys, xs = (t.cpu().numpy() for t in _topk(_t(s, gpu), K=K))
+    esc, eind, ecls, eys, exs = decode_oracle.topk(s, K)
+    np.testing.assert_array_equal(sc, esc)
+    np.testing.assert_array_equal(ind, eind)
+    np.testing.assert_array_equal(cls, ecls)
+    np.testing.assert_array_equal(ys, eys)
+    np.testing.assert_array_equal(xs, exs)
+    assert ind.dtype == np.int64 and cls.dtype == np.int32 and ys.dtype == np.float32
+    B, C, H, W = shape
+    csc, cind, cys, cxs = (t.cpu().numpy() for t in _topk_channel(_t(s, gpu), K=K))
+    assert csc.shape == (B, C, K)
+    flat = s.reshape(B, C, H * W)
+    for b in range(B):
+        for c in range(C):
+            v, i = decode_oracle._topk_desc(flat[b, c], K)
+            np.testing.assert_array_equal(csc[b, c], v)
+            np.testing.assert_array_equal(cind[b, c], i)
+            np.testing.assert_array_equal(cys[b, c], (i // W).astype(np.float32))
+            np.testing.assert_array_equal(cxs[b, c], (i % W).astype(np.float32))
+    with pytest.raises(RuntimeError):
+        _topk(_t(s, gpu), K=H * W + 1)
+
+
+def test_gather_helpers_bit_exact(gpu):
+    from utils.evaluation_utils import _gather_feat, _transpose_and_gather_feat
+    rng = np.random.default_rng(8)
+    feat = rng.standard_normal((3, 4, 21, 19)).astype(np.float32)
+    ind = rng.integers(0, 21 * 19, (3, 37)).astype(np.int64)
+    got = _transpose_and_gather_feat(_t(feat, gpu), _t(ind, gpu)).cpu().numpy()
+    np.testing.assert_array_equal(got, decode_oracle._gather(feat, ind))
+    flat = rng.standard_normal((3, 50, 6)).astype(np.float32)
+    ind2 = rng.integers(0, 50, (3, 11)).astype(np.int64)
+    exp = np.stack([flat[b][ind2[b]] for b in range(3)])
+    np.testing.assert_array_equal(_gather_feat(_t(flat, gpu), _t(ind2, gpu)).cpu().numpy(), exp)
+    # int64 features (the _topk stage-2 gathers of topk_inds), bit for bit
+    big = rng.integers(-2 ** 62, 2 ** 62, (2, 30, 1)).astype(np.int64)
+    ind3 = rng.integers(0, 30, (2, 9)).astype(np.int64)
+    np.testing.assert_array_equal(_gather_feat(_t(big, gpu), _t(ind3, gpu)).cpu().numpy(),
+                                  np.stack([big[b][ind3[b]] for b in range(2)]))
+    with pytest.raises(RuntimeError):
+        _gather_feat(_t(flat, gpu), _t(np.full((3, 2), 50, np.int64), gpu))
+    with pytest.raises(NotImplementedError):
+        _gather_feat(_t(flat, gpu), _t(ind2, gpu), mask=torch.ones((3, 11), dtype=torch.bool, device=gpu))
+
+
+def test_sigmoid_non_contiguous_in_place(gpu):
+    """_sigmoid on a strided view (the reference's in-place sigmoid_ accepts any tensor): the view's
+    elements are updated in place, the rest of the storage is untouched, the same object returned."""
+    from utils.torch_utils import _sigmoid
+    rng = np.random.default_rng(4)
+    base = rng.standard_normal((2, 6, 33, 35)).astype(np.float32)
+    t = _t(base, gpu)
+    view = t[:, 1:5].transpose(2, 3)
+    assert not view.is_contiguous()
+    out = _sigmoid(view)
+    assert out is view
+    exp = base.copy()
+    exp[:, 1:5] = decode_oracle.sigmoid_clamp(base[:, 1:5])
+    got = t.cpu().numpy()
+    np.testing.assert_array_equal(got[:, [0, 5]], base[:, [0, 5]])
+    assert float(np.max(np.abs(got - exp))) <= 2 * np.finfo(np.float32).eps

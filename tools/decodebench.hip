@@ -91,7 +91,7 @@ int main(int argc, char** argv) {
   });
   CK(hipDeviceSynchronize());
   time("old: class_topk (1 block per class)", [&] {
-    hipLaunchKernelGGL(decode_class_topk_kernel, dim3(B * C), dim3(kDecThreads), 0, 0, hm, C, H, W, K, 1, bk, bi);
+    hipLaunchKernelGGL(decode_class_topk_kernel<true>, dim3(B * C), dim3(kDecThreads), 0, 0, hm, C, H, W, K, 1, bk, bi);
   });
   time("old: merge_gather", [&] {
     hipLaunchKernelGGL(decode_merge_gather_kernel, dim3(B), dim3(256), 0, 0, bk, bi, C, K, H, W, 1, off, dr, zz, dm,
