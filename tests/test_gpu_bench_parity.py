@@ -44,6 +44,21 @@ def _run_timed_config(argv, gpu, steps=4):
     return args, b
 
 
+def _check_full_identity(pipe, ref_out, K):
+    """Detections of the timed configuration against the oracle DECODE OF THE ORACLE FORWARD:
+    every frame's (K, 10) rows within 1e-4 — the same peaks, classes and order (the bench line's
+    parity.max_abs_det_err_vs_oracle_forward, asserted)."""
+    hm = decode_oracle.sigmoid_clamp(ref_out["hm_cen"].numpy())
+    off = decode_oracle.sigmoid_clamp(ref_out["cen_offset"].numpy())
+    ref = decode_oracle.decode(hm, off, ref_out["direction"].numpy(), ref_out["z_coor"].numpy(),
+                               ref_out["dim"].numpy(), K=K)
+    got = pipe.dets.cpu().numpy()
+    err = float(np.max(np.abs(got - ref)))
+    assert err <= TOL, err
+    np.testing.assert_array_equal(got[..., 9], ref[..., 9])
+    return err
+
+
 def _check_pipe(pipe, ref_out, K):
     worst = 0.0
     for h in DEFAULT_HEADS:
@@ -72,6 +87,8 @@ def test_bench_bev_infer_config_matches_oracle(gpu):
         ref = model_oracle.forward(_oracle_sd(), torch.from_numpy(x))
     errs = [_check_pipe(p, ref, args.K) for p in b.pipes]
     print("bench bev_infer config: max rel logit err per pipeline", errs)
+    ferrs = [_check_full_identity(p, ref, args.K) for p in b.pipes]
+    print("bench bev_infer config: max abs det err vs the oracle forward's decode", ferrs)
 
 
 def test_bench_e2e_config_matches_oracle(gpu):
@@ -87,3 +104,5 @@ def test_bench_e2e_config_matches_oracle(gpu):
         ref = model_oracle.forward(_oracle_sd(), torch.from_numpy(maps.astype(np.float32)))
     errs = [_check_pipe(p, ref, args.K) for p in b.pipes]
     print("bench e2e config: max rel logit err per pipeline", errs)
+    ferrs = [_check_full_identity(p, ref, args.K) for p in b.pipes]
+    print("bench e2e config: max abs det err vs the oracle forward's decode", ferrs)

@@ -104,24 +104,37 @@ def test_forward_608_end_to_end(golden, gpu):
         np.testing.assert_allclose(o[0][:, ys, xs], g[f"e2e/{h}/samples"], rtol=TOL, atol=TOL)
         assert abs(o.astype(np.float64).sum() - float(g[f"e2e/{h}/sum"])) <= 1e-3 * max(
             1.0, abs(float(g[f"e2e/{h}/sum"])))
+    # the score error the logit error allows: sigmoid' <= 1/4, plus the sigmoid's own rounding
+    hm_abs_err = float(np.max(np.abs(out["hm_cen"].cpu().numpy() - g["e2e/hm_cen/full"])))
+    score_tol = 0.25 * hm_abs_err + 2e-7
     hm = _sigmoid(out["hm_cen"])
     off = _sigmoid(out["cen_offset"])
     dets = decode(hm, off, out["direction"], out["z_coor"], out["dim"], K=50).cpu().numpy()
     ref = g["e2e/dets"]
-    np.testing.assert_allclose(dets, ref, rtol=0, atol=TOL * 100)  # coarse, then exact below
-    score_err = float(np.max(np.abs(np.sort(dets[0, :, 0]) - np.sort(ref[0, :, 0]))))
-    assert score_err <= TOL
-    # identities must agree wherever the reference's ranking is unambiguous
-    s = ref[0, :, 0]
+    # every row whose reference score is separated from its neighbours (and, for the last row,
+    # from the best excluded peak's, which the K-th reference row bounds from above) by more
+    # than twice that error has exactly the reference's identity, and all ten columns within 1e-4
+    s = ref[0, :, 0].astype(np.float64)
     gap_prev = np.r_[np.inf, s[:-1] - s[1:]]
-    gap_next = np.r_[s[:-1] - s[1:], np.inf]
-    safe = (gap_prev > 4 * score_err + 1e-7) & (gap_next > 4 * score_err + 1e-7)
-    assert safe.sum() >= 30
+    gap_next = np.r_[s[:-1] - s[1:], s[-1] - float(g["e2e/top51"][50])]  # the 51st peak (fixture)
+    safe = (gap_prev > 2 * score_tol) & (gap_next > 2 * score_tol)
+    n_amb = int((~safe).sum())
+    print(f"e2e: hm logit abs err {hm_abs_err:.3g}, score tol {score_tol:.3g}: {int(safe.sum())} of 50 rows "
+          f"unambiguous, {n_amb} within the error of a neighbour")
+    assert safe.sum() >= 40
     np.testing.assert_array_equal(dets[0, safe, 9], ref[0, safe, 9])
     np.testing.assert_allclose(dets[0, safe], ref[0, safe], rtol=0, atol=TOL)
+    # the ambiguous rows: the same multiset of scores (a swap of near-equal neighbours only)
+    assert float(np.max(np.abs(np.sort(dets[0, :, 0]) - np.sort(ref[0, :, 0])))) <= score_tol
+    # post_processing: exact per-class counts unless a score lies within the error of peak_thresh
     post = post_processing(dets.copy(), 3, 4, 0.2)
+    near = int(np.sum(np.abs(s - 0.2) <= score_tol))
     for j in range(3):
-        assert abs(len(post[0][j]) - len(g[f"e2e/post_cls{j}"])) <= 1
+        n_ref = len(g[f"e2e/post_cls{j}"])
+        if near == 0:
+            assert len(post[0][j]) == n_ref, j
+        else:
+            assert abs(len(post[0][j]) - n_ref) <= near, j
 
 
 @pytest.mark.parametrize("math", MATHS)
