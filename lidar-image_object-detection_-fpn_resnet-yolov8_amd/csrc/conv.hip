@@ -7,6 +7,7 @@
 #include "conv_h3_kernel.h"
 #include "conv_h3s_kernel.h"
 #include "conv_r3_kernel.h"
+#include "fpn_kernel.h"
 #include "stem_patch_kernel.h"
 
 namespace sfa {
@@ -88,6 +89,22 @@ constexpr int R3_HEAD_STAG = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536 | 5242
 constexpr int H3S_64 = 2 | 4 | 8 | 128;
 constexpr int H3S_128 = 2 | 8;
 
+// FPN 1x1 convs (commuted: the low-resolution W_a . x and the skip conv with the upsampled
+// residual) on the persistent weight-resident kernel (fpn_kernel.h), by channel count.
+static int launch_fpn(const ConvArgs& a, hipStream_t st) {
+  const int C = a.seg[0].C;
+  if (a.res_up) {
+    if (C == 64 && a.N % 64 == 0) return launch_fpn_gemm_cfg<64, 64, true, 3>(a, st);
+    if (C == 128 && a.N % 128 == 0) return launch_fpn_gemm_cfg<128, 128, true, 2>(a, st);
+    if (C == 256 && a.N % 128 == 0) return launch_fpn_gemm_cfg<256, 128, true, 1>(a, st);
+  } else {
+    if (C == 128 && a.N % 64 == 0) return launch_fpn_gemm_cfg<128, 64, false, 4>(a, st);
+    if (C == 256 && a.N % 128 == 0) return launch_fpn_gemm_cfg<256, 128, false, 1>(a, st);
+    if (C == 512 && a.N % 64 == 0) return launch_fpn_gemm_cfg<512, 64, false, 1>(a, st);
+  }
+  return SFA_E_UNSUPPORTED;
+}
+
 static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (!a.wh || !a.winv) return SFA_E_UNSUPPORTED;
   auto ok = [](int rc) { return rc != SFA_E_UNSUPPORTED; };
@@ -99,7 +116,11 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_HEAD, 1, 16, 3, 0, 64, 1>(a, st);  // other head counts
     return rc;
   }
-  if (a.res_up) {  // FPN skip convs: transposed float4 epilogue, float4 taps
+  if (sliced && a.nseg == 1 && a.seg[0].KH == 1 && a.seg[0].KW == 1 && a.seg[0].stride == 1) {
+    rc = launch_fpn(a, st);  // the FPN 1x1 convs (commuted)
+    if (ok(rc)) return rc;
+  }
+  if (a.res_up) {  // FPN skip convs of other widths: conv_r3, transposed float4 epilogue, float4 taps
     if (a.N == 64)
       rc = launch_conv_r3_cfg<128, 64, 32, EPI_STD, 4, 2, R3_FPN>(a, st);
     else if (a.N % 128 == 0)

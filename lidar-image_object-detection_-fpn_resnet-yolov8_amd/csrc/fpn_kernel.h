@@ -1,0 +1,263 @@
+// FPN 1x1 convolutions (fpn_resnet.py:129-131,197-210), fp16x3, as persistent row-streaming GEMMs
+// with the weight slice resident in LDS.
+//
+// conv_up_level{1,2,3} run commuted (model.hip): lo_f = W_a . x at the LOW resolution (no bias),
+// then y = W_b . skip + b + up2x(lo_f) at the high one (the bilinear x2 align_corners upsample of
+// the low-resolution product added in the epilogue: r3t_epilogue_std's res_up path).  Both are
+// GEMMs with a long M (5,776 .. 369,664 rows at bs 16) and a small K x N weight slice (64 x 64 ..
+// 512 x 256): HBM / latency bound, not MFMA bound (a few GFLOP over 50 .. 213 MB).  The
+// per-tile kernels they ran on (conv_r3 / conv_h3: W DMA per K-tile, one 128-row tile per block,
+// 2 .. 16 K-tiles) spent most of a block's life in its prologue and epilogue latencies: 1.7 .. 2.9
+// TB/s.  Here:
+//  * a block loads its BN-column slice of the fp16x3 weight terms ONCE into LDS (K x BN x 4 B:
+//    16 .. 128 KiB; the conv_r3 swizzled fragment layout per 32-wide K-tile) and then walks row
+//    tiles (128 rows: 4 waves x 2 16-row sub-tiles) of the map: grid = CUs x blocks per CU;
+//  * A fragments go straight from HBM into VGPRs (a lane's 8 channels of one pixel per K-tile, as
+//    conv_r3 loads them) in chunks of up to 4 K-tiles, the next chunk (the next tile's first,
+//    across tile boundaries) issued before this chunk's MFMAs;
+//  * the per-frame fp16x3 input scales are read once per block into LDS (rows never re-read the
+//    amax shards);
+//  * products, their order over K (K-tile by K-tile, hi*lo, lo*hi, hi*hi per 16x16x32 MFMA on the
+//    transposed accumulators) and the epilogue are conv_r3_kernel's: the same bits as the conv_r3
+//    FPN launches (R3_FPN) for the skip convs.
+#pragma once
+
+#include "conv_r3_kernel.h"
+
+namespace sfa {
+
+constexpr int kFpnMaxFrames = 256;
+
+// OCC: blocks per CU the launch is built for (__launch_bounds__: 4 -> <= 128 VGPRs, 2 -> 256);
+// the A chunk is 2 K-tiles at 4 blocks per CU, 4 otherwise (two chunks in flight: 2 x KC x TM x 32 B
+// per lane).
+template <int K, int BN, bool RU, int OCC>
+struct FpnGeom {
+  static constexpr int NW = 4, NT = NW * 64, WM = 32, BM = NW * WM, TM = WM / 16, TN = BN / 16;
+  static constexpr int KT = K / 32;                // K-tiles
+  static constexpr int KCM = OCC >= 4 ? 2 : 4;
+  static constexpr int KC = KT < KCM ? KT : KCM;   // K-tiles per A chunk
+  static constexpr int NCH = KT / KC;              // chunks per row tile
+  static constexpr int BROW = 64, TERM_B = BN * BROW, STAGE = 2 * TERM_B, W_BYTES = KT * STAGE;
+  static constexpr int LDS = W_BYTES + kFpnMaxFrames * 4 + 2 * NW * 4;
+  static_assert(K % 32 == 0 && KT % KC == 0 && BN % 16 == 0 && BN >= 16, "fpn geometry");
+};
+
+// r3t_epilogue_std's arithmetic (same rounding sequence: fmaf(acc * ainv, winv, b), + the
+// bilinear tap value, ReLU) one 16-column block at a time, the block's residual taps loaded just
+// before use (sched_barrier between blocks: hoisting every block's taps spilled at <= 128 VGPRs).
+template <int TM, int TN, int NT, bool RU>
+__device__ __forceinline__ void fpn_epilogue(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* red, int mrow0,
+                                             int m0, int n0, int lane, const float (&ainv)[TM]) {
+#pragma clang fp contract(off)
+  const int M = a.M, c16 = lane & 15, g = lane >> 4;
+  AmaxRows am(a.OH * a.OW, m0);
+  int tap[TM][4];
+  float wl[TM][4];
+  if (RU) {
+    const int H = a.OH >> 1, W = a.OW >> 1;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = min(mrow0 + mi * 16 + c16, M - 1);
+      const int ow = m % a.OW, t = m / a.OW;
+      const int oh = t % a.OH, b = t / a.OH;
+      const float fy = a.res_sh * (float)oh, fx = a.res_sw * (float)ow;
+      const int y0 = (int)fy, x0 = (int)fx;
+      const int y1 = y0 + (y0 < H - 1 ? 1 : 0), x1 = x0 + (x0 < W - 1 ? 1 : 0);
+      const float ly1 = fy - (float)y0, lx1 = fx - (float)x0;
+      wl[mi][0] = 1.f - ly1;
+      wl[mi][1] = ly1;
+      wl[mi][2] = 1.f - lx1;
+      wl[mi][3] = lx1;
+      const int fb = b * H * W;
+      tap[mi][0] = (fb + y0 * W + x0) * a.N;
+      tap[mi][1] = (fb + y0 * W + x1) * a.N;
+      tap[mi][2] = (fb + y1 * W + x0) * a.N;
+      tap[mi][3] = (fb + y1 * W + x1) * a.N;
+    }
+  }
+#pragma unroll
+  for (int ni = 0; ni < TN; ++ni) {
+    const int n = n0 + ni * 16 + 4 * g;
+    const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(a.winv + n);
+    const x6_f32x4 bn = a.bias ? *reinterpret_cast<const x6_f32x4*>(a.bias + n) : x6_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = mrow0 + mi * 16 + c16;
+      x6_f32x4 rv = {0.f, 0.f, 0.f, 0.f};
+      if (RU) {
+        const float* r = a.res_up + n;
+        const x6_f32x4 a00 = *reinterpret_cast<const x6_f32x4*>(r + tap[mi][0]);
+        const x6_f32x4 a01 = *reinterpret_cast<const x6_f32x4*>(r + tap[mi][1]);
+        const x6_f32x4 a10 = *reinterpret_cast<const x6_f32x4*>(r + tap[mi][2]);
+        const x6_f32x4 a11 = *reinterpret_cast<const x6_f32x4*>(r + tap[mi][3]);
+        const float ly0 = wl[mi][0], ly1 = wl[mi][1], lx0 = wl[mi][2], lx1 = wl[mi][3];
+#pragma unroll
+        for (int v = 0; v < 4; ++v)
+          rv[v] = fmaf(ly0, fmaf(lx0, a00[v], lx1 * a01[v]), ly1 * fmaf(lx0, a10[v], lx1 * a11[v]));
+      }
+      x6_f32x4 val;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float t = fmaf(acc[mi][ni][v] * ainv[mi], cs[v], bn[v]);
+        if (RU) t += rv[v];
+        if (a.relu) t = fmaxf(t, 0.f);
+        val[v] = t;
+      }
+      if (m < M) {
+        *reinterpret_cast<x6_f32x4*>(a.y + (size_t)m * a.N + n) = val;
+        if (a.amax_out)
+          am.add(a.amax_out, m, fmaxf(fmaxf(fabsf(val[0]), fabsf(val[1])), fmaxf(fabsf(val[2]), fabsf(val[3]))));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (a.amax_out) amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1, reinterpret_cast<float*>(red));
+}
+
+template <int K, int BN, bool RU, int OCC>
+__global__ void __launch_bounds__(256, OCC) fpn_gemm_kernel(const ConvArgs a, int n_mt) {
+  using G = FpnGeom<K, BN, RU, OCC>;
+  constexpr int NW = G::NW, NT = G::NT, WM = G::WM, BM = G::BM, TM = G::TM, TN = G::TN;
+  constexpr int KC = G::KC, NCH = G::NCH, BROW = G::BROW, TERM_B = G::TERM_B, STAGE = G::STAGE;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[G::LDS];
+  float* const FS = reinterpret_cast<float*>(smem + G::W_BYTES);  // per-frame fp16x3 scales
+  unsigned char* const RED = smem + G::W_BYTES + kFpnMaxFrames * 4;  // epilogue amax reduction
+  auto swzB = [](int R) { return ((R >> 2) & 3) ^ ((((R & 15) + 4) >> 3) & 1); };
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c16 = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.y * BN;
+  const int M = a.M, P = a.OH * a.OW, nframes = (M + P - 1) / P;
+
+  // the weight slice (columns n0 .. n0 + BN - 1, K columns from wk0) and the frame scales -> LDS
+  {
+    const int wst = a.wstride ? a.wstride : a.Kpad;
+    const size_t term_elems = (size_t)a.N * wst;
+    for (int c = tid; c < G::KT * 2 * BN * 4; c += NT) {
+      const int q = c & 3, n = (c >> 2) % BN, rest = (c >> 2) / BN, term = rest & 1, kt = rest >> 1;
+      const r3_u32x4 v = *reinterpret_cast<const r3_u32x4*>(a.wh + term * term_elems + (size_t)(n0 + n) * wst + a.wk0 +
+                                                           kt * 32 + 8 * q);
+      *reinterpret_cast<r3_u32x4*>(smem + kt * STAGE + term * TERM_B + n * BROW + ((q ^ swzB(n)) << 4)) = v;
+    }
+    for (int f = tid; f < nframes; f += NT) {
+      float sinv;
+      FS[f] = amax_frame_scale(a.amax_in, 1, f, sinv);
+    }
+  }
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.seg[0].x), (short)0,
+                                                                       (int)a.seg[0].bytes, 0x00020000);
+  const int bfo = c16 * BROW + ((g ^ swzB(c16)) << 4);
+  const int n_my = blockIdx.x < n_mt ? (n_mt - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int steps = n_my * NCH;
+
+  r3_u32x4 ra[KC][TM][2], rb[KC][TM][2];  // A chunks, ping-pong
+  auto load = [&](int step, r3_u32x4 (&r)[KC][TM][2]) {
+    const int t = step / NCH, c = step - t * NCH;
+    const int m0 = ((int)blockIdx.x + t * (int)gridDim.x) * BM;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = m0 + wave * WM + mi * 16 + c16;
+      const unsigned base = m < M ? (unsigned)(((size_t)m * K + (size_t)c * KC * 32 + 8 * g) * 4) : 0x80000000u;
+#pragma unroll
+      for (int kk = 0; kk < KC; ++kk) {
+        const unsigned off = base == 0x80000000u ? base : base + kk * 128u;
+        r[kk][mi][0] = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
+        r[kk][mi][1] = __builtin_amdgcn_raw_buffer_load_b128(rsx, off + 16u, 0, 0);
+      }
+    }
+  };
+  f32x4_t acc[TM][TN];
+  float as[TM], ainv[TM];
+  auto process = [&](int step, r3_u32x4 (&r)[KC][TM][2]) {
+    const int t = step / NCH, c = step - t * NCH;
+    const int m0 = ((int)blockIdx.x + t * (int)gridDim.x) * BM;
+    if (c == 0) {
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        const int m = min(m0 + wave * WM + mi * 16 + c16, M - 1);
+        as[mi] = FS[m / P];
+        ainv[mi] = 1.f / as[mi];
+#pragma unroll
+        for (int ni = 0; ni < TN; ++ni) acc[mi][ni] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int kk = 0; kk < KC; ++kk) {
+      f16x8_t hf[2][TM];
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi)
+        split2h_x8(__builtin_bit_cast(x6_f32x4, r[kk][mi][0]), __builtin_bit_cast(x6_f32x4, r[kk][mi][1]), as[mi],
+                   hf[0][mi], hf[1][mi]);
+      const unsigned char* S = smem + (c * KC + kk) * STAGE;
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const f16x8_t c0 = *reinterpret_cast<const f16x8_t*>(S + bfo + ni * 16 * BROW);
+        const f16x8_t c1 = *reinterpret_cast<const f16x8_t*>(S + TERM_B + bfo + ni * 16 * BROW);
+#pragma unroll
+        for (int mi = 0; mi < TM; ++mi) {
+          f32x4_t cc = acc[mi][ni];
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[1][mi], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c1, hf[0][mi], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[0][mi], cc, 0, 0, 0);
+          acc[mi][ni] = cc;
+        }
+      }
+    }
+    if (c == NCH - 1) fpn_epilogue<TM, TN, NT, RU>(a, acc, RED, m0 + wave * WM, m0, n0, lane, ainv);
+  };
+  // two chunks in flight: the next one's loads issued before this one's MFMAs; one copy of the
+  // body (rb is moved into ra, which the next iteration's MFMAs would wait for anyway)
+  if (steps > 0) load(0, ra);
+  for (int s = 0; s < steps; ++s) {
+    if (s + 1 < steps) load(s + 1, rb);
+    process(s, ra);
+#pragma unroll
+    for (int kk = 0; kk < KC; ++kk)
+#pragma unroll
+      for (int mi = 0; mi < TM; ++mi) {
+        ra[kk][mi][0] = rb[kk][mi][0];
+        ra[kk][mi][1] = rb[kk][mi][1];
+      }
+  }
+}
+
+// One FPN 1x1 conv (one segment, 1x1 / stride 1, K = its channel count, weight slice by
+// wstride / wk0, optional half-resolution residual res_up); SFA_E_UNSUPPORTED for other shapes.
+template <int K, int BN, bool RU, int OCC>
+inline int launch_fpn_gemm_cfg(const ConvArgs& a, hipStream_t st) {
+  using G = FpnGeom<K, BN, RU, OCC>;
+  static_assert(OCC * G::LDS <= 160 * 1024, "blocks per CU vs LDS");
+  const ConvSeg& g = a.seg[0];
+  if (a.nseg != 1 || g.KH != 1 || g.KW != 1 || g.stride != 1 || g.pad != 0 || g.C != K || a.Kpad != K ||
+      a.N % BN != 0 || !a.wh || !a.winv || a.res || a.ksplit > 1 || a.OH != g.H || a.OW != g.W ||
+      (a.res_up != nullptr) != RU || (a.wstride && (a.wstride < a.wk0 + K || a.wk0 % 8 != 0))) {
+    set_error("fpn_gemm: not a 1x1 conv with C = %d (N=%d)", K, a.N);
+    return SFA_E_UNSUPPORTED;
+  }
+  const int P = a.OH * a.OW;
+  if ((a.M + P - 1) / P > kFpnMaxFrames || 2ull * a.N * (a.wstride ? a.wstride : a.Kpad) * 2ull >= (1ull << 31)) {
+    set_error("fpn_gemm: more than %d frames or weights >= 2 GiB", kFpnMaxFrames);
+    return SFA_E_UNSUPPORTED;
+  }
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  const int n_mt = ceil_div(a.M, G::BM), n_nt = a.N / BN;
+  int gx = (ncu * OCC + n_nt - 1) / n_nt;  // blocks per column tile
+  if (gx > n_mt) gx = n_mt;
+  if (gx < 1) return SFA_OK;
+  hipLaunchKernelGGL((fpn_gemm_kernel<K, BN, RU, OCC>), dim3((unsigned)gx, (unsigned)n_nt), dim3(G::NT), 0, st, a,
+                     n_mt);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+}  // namespace sfa

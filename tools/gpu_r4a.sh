@@ -16,4 +16,8 @@ for w in "bev_infer" "stream" "fusion --batch 8"; do
   timeout -k 10 300 python bench.py --gpus 2 --steps 10 --warmup 3 --workload $w > gpurun_out/g2_$TAG.json 2> gpurun_out/g2_$TAG.err || { echo "self-launched gloo rehearsal failed: $w"; tail -20 gpurun_out/g2_$TAG.err; exit 1; }
   python3 -c "import json,sys; L=[l for l in open('gpurun_out/g2_$TAG.json') if l.startswith('{')]; assert len(L)==1, L; d=json.loads(L[0]); print(sys.argv[1], d['n_gpus'], d['value'], d['config']['workload'][:120])" "$w"
 done
+
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --inflight 1 --serial-heads --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bp_$TAG.json 2> gpurun_out/bp_$TAG.err || { echo "rocprof failed"; tail gpurun_out/bp_$TAG.err; exit 1; }
+KT=$(find gpurun_out/prof_$TAG -name "*kernel_trace.csv" -print -quit); python3 tools/rocprof_summary.py "$KT" > gpurun_out/prof_summary_$TAG.txt 2>&1 || true
+head -30 gpurun_out/prof_summary_$TAG.txt
 echo done
