@@ -22,6 +22,11 @@ def run(out):
     import torch
     from sfa_hip import _lib, runtime, synthetic
     _lib.ABI_VERSION = int(os.environ.get("SFA_ABI_EXPECT", _lib.ABI_VERSION))
+    import ctypes
+    probe = ctypes.CDLL(_lib.LIB_PATH)  # an older build lacks the newer entry points: bind what it has
+    for name in [n for n in _lib._PROTOS if not hasattr(probe, n)]:
+        print("not in", _lib.LIB_PATH, ":", name)
+        del _lib._PROTOS[name]
     dev = torch.device("cuda", 0)
     arch = _lib.make_arch(runtime.DEFAULT_HEADS)
     sd = synthetic.synthetic_state_dict(_lib.state_layout(arch), 0)
