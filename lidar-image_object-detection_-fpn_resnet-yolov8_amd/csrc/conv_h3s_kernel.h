@@ -32,6 +32,10 @@ namespace sfa {
 // One f32 strip buffer: the next strip is issued at kw 1, when every wave has split this one.
 // 128 = (with 4) the residual tile loaded at the last super-step's kw 1 (in place of the no-op
 // strip reload), so the last six k-steps' MFMAs hide its latency; 2 and 8 are always set.
+// 256 = register-staged W (round 4): each k-step's W pieces are fetched with buffer_load_dwordx4
+// into VGPRs at the step's start and written to the other W stage with ds_write_b128 after the
+// step's MFMAs (an LDS-DMA piece costs ~60 issue cycles, a load + ds_write_b128 ~20); same
+// LDS image, same products: bit-identical.
 template <int BM, int BN, int WM, int EPI, int OCC, int ABL = 0>
 __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const ConvArgs a) {
   constexpr int NW = BM / WM, NT = NW * 64;
@@ -46,13 +50,14 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
   constexpr int NB = (ND_B + NW - 1) / NW, NB_REM = ND_B % NW;
   constexpr bool PS = (ABL & 4) != 0;
   constexpr bool RESPF = PS && (ABL & 128) != 0;
+  constexpr bool RW = (ABL & 256) != 0;
   constexpr int PROWS = WM + 2;              // a wave's pre-split rows (its WM rows + the kw halo)
   constexpr int PR_BYTES = (PROWS + 1) * 64;  // per term: 32 fp16 per row, + one zero row
   constexpr int NSB = PS ? 1 : 2;             // f32 strip buffers
   constexpr int MAIN_BYTES = NSB * S_BYTES + 2 * W_BYTES + (PS ? NW * 2 * PR_BYTES : 0);
   constexpr int LDS_BYTES = MAIN_BYTES;
   static_assert(NW % 2 == 0 && WM % 16 == 0 && BN % 16 == 0, "tile");
-  static_assert((ABL & 10) == 10 && (ABL & ~(2 | 4 | 8 | 128)) == 0, "product strip-kernel form (see the bit list)");
+  static_assert((ABL & 10) == 10 && (ABL & ~(2 | 4 | 8 | 128 | 256)) == 0, "product strip-kernel form (see the bit list)");
   static_assert(EPI == EPI_STD, "transposed form: standard epilogue only");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
 
@@ -149,6 +154,27 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
             (unsigned)(boff[jj] + 2 * k0), 0, 0, 0);
     }
   };
+  x6_u32x4 wreg[NB];  // RW: the next k-step's W pieces
+  auto load_w_regs = [&](int k0) {
+#pragma unroll
+    for (int jj = 0; jj < NB; ++jj) {
+      if (NB_REM == 0 || jj < NB - 1 || wave < NB_REM)
+        wreg[jj] = __builtin_amdgcn_raw_buffer_load_b128(rsw, (unsigned)(boff[jj] + 2 * k0), 0, 0);
+    }
+  };
+  auto store_w_regs = [&](unsigned char* S) {
+#pragma unroll
+    for (int jj = 0; jj < NB; ++jj) {
+      if (NB_REM == 0 || jj < NB - 1 || wave < NB_REM)
+        *reinterpret_cast<x6_u32x4*>(S + (wave + NW * jj) * 1024 + lane * 16) = wreg[jj];
+    }
+  };
+  // RW: wait for this wave's W loads (every vector-memory op issued after them may still fly)
+  auto wait_w_regs = [&](int younger) {
+    if (younger == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (NS_REM == 0 || wave < NS_REM) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS - 1) : "memory");
+  };
   auto wk0 = [&](int s, int kw) {  // K offset of the W tile of super-step s, tap kw
     const int kh = s / nchunk, c0 = (s - kh * nchunk) << 5;
     return (kh * 3 + kw) * g.C + c0;
@@ -237,8 +263,15 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
   };
 
   unsigned char* const WB = smem + NSB * S_BYTES;
-  load_strip(s0, smem);
-  load_w(wk0(s0, 0), WB);
+  if constexpr (RW) {
+    load_w_regs(wk0(s0, 0));
+    load_strip(s0, smem);
+    wait_w_regs(1);
+    store_w_regs(WB);
+  } else {
+    load_strip(s0, smem);
+    load_w(wk0(s0, 0), WB);
+  }
   for (int sl = 0; sl < nsl; ++sl) {
     const int s = s0 + sl;
     const bool last = sl + 1 == nsl;
@@ -260,19 +293,28 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
+        if constexpr (RW) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // W(t) stores
         __builtin_amdgcn_s_barrier();
         const int wnext = kw < 2 ? wk0(s, kw + 1) : (last ? wk0(s, 2) : wk0(s + 1, 0));
         unsigned char* const wdst = WB + ((t + 1) & 1) * W_BYTES;
-        load_w(wnext, wdst);
+        if constexpr (RW) load_w_regs(wnext);
+        else load_w(wnext, wdst);
+        bool strip_after = false;
         if (kw == 1) {
           if (RESPF && last) {  // the residual tile (the last MFMAs hide its latency)
             if (a.res && nsplit == 1) r3t_res_load<TM, TN>(a, rvp, m0 + wave * WM, n0, lane);
           } else {
             load_strip(last ? s : s + 1, smem);  // every wave has split strip s
+            strip_after = true;
           }
         }
         if (kw == 0) presplit(smem);
         compute(smem, WB + (t & 1) * W_BYTES, kw);
+        if constexpr (RW) {
+          if (RESPF && last && kw == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          else wait_w_regs(strip_after ? 1 : 0);
+          store_w_regs(wdst);
+        }
         continue;
       }
       if (kw == 1) {
@@ -283,13 +325,19 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      if constexpr (RW) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // W(t) stores
       __builtin_amdgcn_s_barrier();  // W(t) (and the strip) landed for every wave; W(t-1) no longer read
       const int wnext = kw < 2 ? wk0(s, kw + 1) : (last ? wk0(s, 2) : wk0(s + 1, 0));
       unsigned char* const wdst = WB + ((t + 1) & 1) * W_BYTES;
       unsigned char* const sdst = smem + ((sl + 1) & 1) * S_BYTES;
-      load_w(wnext, wdst);
+      if constexpr (RW) load_w_regs(wnext);
+      else load_w(wnext, wdst);
       if (kw == 0) load_strip(last ? s : s + 1, sdst);
       compute(smem + (sl & 1) * S_BYTES, WB + (t & 1) * W_BYTES, kw);
+      if constexpr (RW) {
+        wait_w_regs(kw == 0 ? 1 : 0);
+        store_w_regs(wdst);
+      }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -20,4 +20,6 @@ done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python bench.py --inflight 1 --serial-heads --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/bp_$TAG.json 2> gpurun_out/bp_$TAG.err || { echo "rocprof failed"; tail gpurun_out/bp_$TAG.err; exit 1; }
 KT=$(find gpurun_out/prof_$TAG -name "*kernel_trace.csv" -print -quit); python3 tools/rocprof_summary.py "$KT" > gpurun_out/prof_summary_$TAG.txt 2>&1 || true
 head -30 gpurun_out/prof_summary_$TAG.txt
+timeout -k 10 300 ./tools/convbench4 20 > gpurun_out/cb4_$TAG.txt 2>&1 || { echo "convbench4 failed"; tail gpurun_out/cb4_$TAG.txt; exit 1; }
+grep -E "==|us " gpurun_out/cb4_$TAG.txt
 echo done
