@@ -22,6 +22,7 @@
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3s_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_r3_kernel.h"
+#include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/stem_band_kernel.h"
 
 namespace sfa {
 void set_error(const char* fmt, ...) {
@@ -140,6 +141,17 @@ static const size_t g_part_floats = 64u << 20;
           return launch_conv_h3s_cfg<BM, BN, WM, EPI, OCC, ABL>(b, s);                            \
         }                                                                                         \
   }
+// the fp16x3 stems (NCHW3 input planes, pooled output): band kernel / round-3 patch kernel + merge
+#define CANDSTEM(FORM)                                                                            \
+  Cand {                                                                                          \
+    FORM == 2 ? "h3 stem band" : "h3 stem patch+merge", 32, [](const ConvArgs& a, hipStream_t s) { \
+      ConvArgs b = a;                                                                             \
+      b.stem_in = STEM_IN_NCHW3;                                                                  \
+      b.part = g_part;                                                                            \
+      b.part_floats = g_part_floats;                                                              \
+      return FORM == 2 ? launch_stem_band(b, s) : launch_stem_patch_pool(b, s);                  \
+    }                                                                                             \
+  }
 #define CANDR(BM, BN, WM, EPI, OCC, NS, ABL, KS)                                                    \
   Cand {                                                                                          \
     "h3r " #BM "x" #BN " w" #WM " occ" #OCC " st" #NS " abl" #ABL " ks" #KS, 32,                    \
@@ -174,7 +186,7 @@ int main(int argc, char** argv) {
       CANDTK(128, 64, 32, EPI_STD, 3, 142, 1), CANDTK(128, 64, 32, EPI_STD, 3, 398, 1),
       CANDTK(128, 64, 32, EPI_STD, 3, 142, 1), CANDTK(128, 64, 32, EPI_STD, 3, 398, 1),
   };
-  std::vector<Cand> stem = {};
+  std::vector<Cand> stem = {CANDSTEM(1), CANDSTEM(2), CANDSTEM(1), CANDSTEM(2)};
   std::vector<Cand> nbig = {
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 1), CANDTK(128, 128, 32, EPI_STD, 2, 266, 1),
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 1), CANDTK(128, 128, 32, EPI_STD, 2, 266, 1),

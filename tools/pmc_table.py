@@ -7,7 +7,10 @@ def load(d):
     rows = collections.OrderedDict()
     f = os.path.join(d, "run_counter_collection.csv")
     if not os.path.exists(f):
-        return rows
+        found = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if not found:
+            return rows
+        f = found[0]
     for r in csv.DictReader(open(f)):
         key = int(r["Dispatch_Id"])
         name = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "")
