@@ -190,10 +190,14 @@ int main(int argc, char** argv) {
   std::vector<Cand> nbig = {
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 1), CANDTK(128, 128, 32, EPI_STD, 2, 266, 1),
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 1), CANDTK(128, 128, 32, EPI_STD, 2, 266, 1),
+      CANDTK(64, 128, 16, EPI_STD, 3, 10, 1), CANDTK(128, 64, 32, EPI_STD, 3, 10, 1),
   };
   std::vector<Cand> n512 = {
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 2), CANDTK(128, 128, 32, EPI_STD, 2, 266, 2),
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 2), CANDTK(128, 128, 32, EPI_STD, 2, 266, 2),
+      // round 4: grids that fill the chip without split-K (no reduce launch)
+      CANDTK(64, 128, 16, EPI_STD, 3, 10, 1), CANDTK(128, 64, 32, EPI_STD, 3, 10, 1),
+      CANDTK(128, 64, 32, EPI_STD, 3, 142, 1),
   };
   std::vector<Cand> heads = {
       CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1),
