@@ -196,6 +196,9 @@ struct ConvArgs {
   // (the reference's (B, 3, H, W)), STEM_IN_NCHW3_FLIP (read as torch.flip(x, [2, 3])); every
   // 16 x 16 output tile scales its fp16x3 patch by its own max |x| (no layout / amax pass).
   int stem_in;
+  // FPN 1x1 convs: 1 = may run on the persistent weight-resident kernel (fpn_kernel.h), 0 = the
+  // per-tile conv_h3 / conv_r3 kernels (model option SFA_OPT_FPN_GEMM)
+  int fpn_gemm;
 };
 
 // Bilinear x2 (align_corners) sample of a half-resolution NHWC tensor at output pixel

@@ -116,7 +116,7 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     if (!ok(rc)) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_HEAD, 1, 16, 3, 0, 64, 1>(a, st);  // other head counts
     return rc;
   }
-  if (sliced && a.nseg == 1 && a.seg[0].KH == 1 && a.seg[0].KW == 1 && a.seg[0].stride == 1) {
+  if (a.fpn_gemm && sliced && a.nseg == 1 && a.seg[0].KH == 1 && a.seg[0].KW == 1 && a.seg[0].stride == 1) {
     rc = launch_fpn(a, st);  // the FPN 1x1 convs (commuted)
     if (ok(rc)) return rc;
   }

@@ -283,11 +283,16 @@ struct sfa_model {
   Plan plan;
   int math;
   int fpn_commute = 7;  // fp16x3: bit f -> FPN conv f as up(W_a x) + W_b skip (env SFA_FPN_COMMUTE, mask)
-  // fp16x3 stem form (env SFA_STEM_PATCH): 2 = full-width band kernel, pool in the epilogue, no
-  // merge pass (stem_band_kernel.h; shapes it does not take use 1); 1 = the round-3 16 x 16 patch
-  // kernel + its merge pass (stem_patch_kernel.h); 0 = the implicit-GEMM stem conv + the max-pool
-  // kernel, as the other math modes
-  int stem_patch = 2;
+  // fp16x3 stem form (env SFA_STEM_PATCH): 1 (default) = the 16 x 16 patch kernel + its merge pass
+  // (stem_patch_kernel.h); 2 = the full-width band kernel, pool in the epilogue, no merge pass
+  // (stem_band_kernel.h; shapes it does not take use 1 — measured 196-212 us against the patch
+  // stem's 170-177 + merge, profiles/r04a_*, so not the default); 0 = the implicit-GEMM stem conv +
+  // the max-pool kernel, as the other math modes
+  int stem_patch = 1;
+  // fp16x3 FPN 1x1 convs on the persistent weight-resident kernel (fpn_kernel.h), mask (env
+  // SFA_FPN_GEMM): bit f = level f's low-resolution W_a . x conv, bit 3 + f = its skip conv with the
+  // upsampled residual; the other convs run on conv_h3 / conv_r3 (same products for the skip convs)
+  int fpn_gemm = 5;
   // Side stream for the level-0 heads (they only need up_level2, so they overlap the rest
   // of the FPN and the level-1/2 heads); created with the model on the current device,
   // used only when the forward's stream is on that device.
@@ -468,6 +473,7 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   // overrides them; nothing reads the environment on the launch path)
   if (const char* e = getenv("SFA_STEM_PATCH")) m->stem_patch = atoi(e) < 0 ? 0 : (atoi(e) > 2 ? 2 : atoi(e));
   if (const char* e = getenv("SFA_FPN_COMMUTE")) m->fpn_commute = atoi(e) & 7;
+  if (const char* e = getenv("SFA_FPN_GEMM")) m->fpn_gemm = atoi(e) & 63;
   bool side_streams = true;  // env SFA_SIDE_STREAMS=0: every launch on the caller's stream (A/B)
   if (const char* e = getenv("SFA_SIDE_STREAMS")) side_streams = strcmp(e, "0") != 0;
   if (side_streams) make_side_streams(m);
@@ -510,6 +516,10 @@ extern "C" int sfa_model_set_option(sfa_model* model, int key, int value) {
       SFA_CHECK_ARG(value >= 0 && value <= 7, "set_option: FPN_COMMUTE mask %d not in 0..7", value);
       model->fpn_commute = value;
       break;
+    case SFA_OPT_FPN_GEMM:
+      SFA_CHECK_ARG(value >= 0 && value <= 63, "set_option: FPN_GEMM mask %d not in 0..63", value);
+      model->fpn_gemm = value;
+      break;
     default: set_error("set_option: unknown key %d", key); return SFA_E_INVALID;
   }
   return SFA_OK;
@@ -520,6 +530,7 @@ extern "C" int sfa_model_get_option(const sfa_model* model, int key, int* value)
   switch (key) {
     case SFA_OPT_STEM_PATCH: *value = model->stem_patch; break;
     case SFA_OPT_FPN_COMMUTE: *value = model->fpn_commute; break;
+    case SFA_OPT_FPN_GEMM: *value = model->fpn_gemm; break;
     default: set_error("get_option: unknown key %d", key); return SFA_E_INVALID;
   }
   return SFA_OK;
@@ -807,6 +818,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       a.wstride = pc.Kpad;
       a.wk0 = 0;
       a.seg[0] = seg(x, B, xh, xw, xc, 1, 1, 0);
+      a.fpn_gemm = (m->fpn_gemm >> f) & 1;
       io(a, xslot_in, -1, -1);
       SFA_RC(launch_conv(a, EPI_STD, m->math, fs));
     }
@@ -818,6 +830,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     a.res_up = fpn_lo[f];
     a.res_sh = xh > 1 ? (float)(xh - 1) / (float)(2 * xh - 1) : 0.f;
     a.res_sw = xw > 1 ? (float)(xw - 1) / (float)(2 * xw - 1) : 0.f;
+    a.fpn_gemm = (m->fpn_gemm >> (3 + f)) & 1;
     io(a, skip_slot, -1, out_slot);
     return launch_conv(a, EPI_STD, m->math, fs);
   };

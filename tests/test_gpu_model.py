@@ -311,6 +311,40 @@ def test_fpn_commute_matches_concat_conv(golden, gpu):
         assert float(np.max(np.abs(outs[0][h] - r) / scale)) <= 1e-4, h
 
 
+@pytest.mark.parametrize("hw", [(160, 192), (608, 608)])
+def test_fpn_gemm_kernel_choices(golden, gpu, hw):
+    """SFA_OPT_FPN_GEMM: the commuted FPN 1x1 convs on the persistent weight-resident kernel
+    (fpn_kernel.h) or on the per-tile kernels. The skip convs (upsampled residual) form the same
+    products in the same order as conv_r3: bit-identical (mask 56 vs 0); the low-resolution convs
+    (conv_h3's K order differs) agree to f32 rounding; every mask within 1e-4 of the CPU reference
+    at 160 x 192."""
+    from oracle import model_oracle
+    x = torch.from_numpy(synthetic.synthetic_bev(2, hw[0], hw[1], seed=19)).to(gpu)
+    res = {}
+    for mask in (0, 56, 7, 63, 5):
+        model = make_model(golden, gpu)
+        eng = model._engine(gpu)
+        eng.set_math(_math("fp16x3"))
+        eng.set_option(_lib.OPT_FPN_GEMM, mask)
+        assert eng.get_option(_lib.OPT_FPN_GEMM) == mask
+        with torch.no_grad():
+            res[mask] = {h: v.cpu().numpy() for h, v in model(x).items()}
+    ref = None
+    if hw == (160, 192):
+        sd = gc.state_dict_np(golden.model)
+        ref = model_oracle.forward(model_oracle.state_dict_torch(sd), x.cpu(), dict(gc.HEADS))
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(res[56][h], res[0][h], err_msg=f"{h}: skip convs fpn_gemm vs conv_r3")
+        np.testing.assert_array_equal(res[63][h], res[7][h], err_msg=f"{h}: skip convs fpn_gemm vs conv_r3")
+        scale = np.maximum(1.0, np.abs(res[0][h]))
+        for mask in (7, 63, 5):
+            assert float(np.max(np.abs(res[mask][h] - res[0][h]) / scale)) <= 2e-5, (h, mask)
+        if ref is not None:
+            r = ref[h].numpy()
+            for mask in res:
+                assert float(np.max(np.abs(res[mask][h] - r) / np.maximum(1.0, np.abs(r)))) <= 1e-4, (h, mask)
+
+
 def test_batch_invariance_608(golden, gpu):
     """At the full 608x608 size (every kernel path of the bench: r3 heads, strip convs, FPN skip
     convs, r3 body convs (M >= 50000 needs >= 9 frames), split-K layer4): frames 7, 8 of a batch
