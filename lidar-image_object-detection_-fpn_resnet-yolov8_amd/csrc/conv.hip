@@ -9,6 +9,7 @@
 #include "conv_r3_kernel.h"
 #include "fpn_kernel.h"
 #include "stem_band_kernel.h"
+#include "conv_ws_kernel.h"
 
 namespace sfa {
 
@@ -66,7 +67,7 @@ static bool strip_ok(const ConvArgs& a) {
 //  * 3x3/s1 body convs: conv_h3s_kernel (A staged once per kh as a row strip for the three kw
 //    taps), transposed float4 epilogue, v_fma_mix split; 64-wide 128 x 64 at 3 blocks / CU with the
 //    pre-split strip and the residual loaded during the last super-step, 128..512-wide 128 x 128
-//    (split-K 2 for the 512-wide);
+//    (split-K 2 for the 512-wide; the 256-wide layer3 convs on 64 x 128 tiles);
 //  * big-M (layer2) stride-2 and conv + downsample convs: conv_r3_kernel 128 x 128 (A in registers,
 //    chunk-major K), -25 % on layer2.0.conv1 against conv_h3;
 //  * FPN skip convs (half-resolution residual added bilinearly upsampled in the epilogue):
@@ -128,7 +129,8 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     return rc;
   }
   if (a.N == 64) {
-    if (strip) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, H3S_64>(a, st);
+    if (strip && a.conv_ws) rc = launch_conv_ws(a, st);  // weight-stationary, full-width rows
+    if (!ok(rc) && strip) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, H3S_64>(a, st);
     if (!ok(rc) && a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 64, 32, EPI_STD, 2, 16, 3, false, 0>(a, st);
     if (!ok(rc) && !sliced) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_STD, 1, 16, 3, 0, 64, 1>(a, st);
@@ -137,7 +139,12 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
   if (a.N % 128 == 0) {
     ConvArgs b = a;
     b.ksplit = pick_ksplit(a);
-    if (strip && (3 * (a.seg[0].C >> 5)) % b.ksplit == 0)
+    if (strip && b.ksplit == 1 && a.N == 256 && tile_rows(a) < 50000)
+      // layer3 (362 128-row tiles for 512 block slots): 64 x 128 tiles at 3 blocks / CU fill the
+      // chip; same per-element K order, so the same bits (tools/convbench4: 97.7 vs 102.0 us,
+      // profiles/r04a_convbench4_stem_regw_tiles.txt)
+      rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3, H3S_128>(b, st);
+    else if (strip && (3 * (a.seg[0].C >> 5)) % b.ksplit == 0)
       rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, H3S_128>(b, st);
     else if (!strip && tile_rows(a) >= 50000)  // big-M stride-2 / two-segment: A from registers
       rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);

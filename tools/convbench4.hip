@@ -18,6 +18,7 @@
 #include <thread>
 
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_kernel.h"
+#include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_ws_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_x6_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3s_kernel.h"
@@ -186,6 +187,8 @@ int main(int argc, char** argv) {
       CANDTK(128, 64, 32, EPI_STD, 3, 142, 1), CANDTK(128, 64, 32, EPI_STD, 3, 398, 1),
       CANDTK(128, 64, 32, EPI_STD, 3, 142, 1), CANDTK(128, 64, 32, EPI_STD, 3, 398, 1),
   };
+  n64.push_back(Cand{"h3 weight-stationary rows", 32, [](const ConvArgs& a, hipStream_t s) { return launch_conv_ws(a, s); }});
+  n64.push_back(Cand{"h3 weight-stationary rows", 32, [](const ConvArgs& a, hipStream_t s) { return launch_conv_ws(a, s); }});
   std::vector<Cand> stem = {CANDSTEM(1), CANDSTEM(2), CANDSTEM(1), CANDSTEM(2)};
   std::vector<Cand> nbig = {
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 1), CANDTK(128, 128, 32, EPI_STD, 2, 266, 1),
