@@ -176,10 +176,8 @@ int sfa_model_get_math(const sfa_model* model);
  *                                         weight-resident kernel: bit f = level f's low-resolution
  *                                         conv, bit 3 + f = its skip conv (5: the low-res convs of
  *                                         levels 0 and 2); the others on the per-tile kernels
- *   SFA_OPT_CONV_WS     (SFA_CONV_WS)     1: the 64 -> 64 3x3 convs (layer1) on the weight-stationary
- *                                         full-row kernel; 0: the strip kernel (the same bits)
  */
-enum sfa_model_option { SFA_OPT_STEM_PATCH = 0, SFA_OPT_FPN_COMMUTE = 1, SFA_OPT_FPN_GEMM = 2, SFA_OPT_CONV_WS = 3 };
+enum sfa_model_option { SFA_OPT_STEM_PATCH = 0, SFA_OPT_FPN_COMMUTE = 1, SFA_OPT_FPN_GEMM = 2 };
 int sfa_model_set_option(sfa_model* model, int key, int value);
 int sfa_model_get_option(const sfa_model* model, int key, int* value);
 

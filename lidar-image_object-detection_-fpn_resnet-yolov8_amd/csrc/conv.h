@@ -199,9 +199,6 @@ struct ConvArgs {
   // FPN 1x1 convs: 1 = may run on the persistent weight-resident kernel (fpn_kernel.h), 0 = the
   // per-tile conv_h3 / conv_r3 kernels (model option SFA_OPT_FPN_GEMM)
   int fpn_gemm;
-  // 64 -> 64 3x3/s1 convs: 1 = may run on the weight-stationary kernel (conv_ws_kernel.h), 0 = the
-  // strip kernel (model option SFA_OPT_CONV_WS)
-  int conv_ws;
 };
 
 // Bilinear x2 (align_corners) sample of a half-resolution NHWC tensor at output pixel

@@ -9,7 +9,6 @@
 #include "conv_r3_kernel.h"
 #include "fpn_kernel.h"
 #include "stem_band_kernel.h"
-#include "conv_ws_kernel.h"
 
 namespace sfa {
 
@@ -129,8 +128,7 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     return rc;
   }
   if (a.N == 64) {
-    if (strip && a.conv_ws) rc = launch_conv_ws(a, st);  // weight-stationary, full-width rows
-    if (!ok(rc) && strip) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, H3S_64>(a, st);
+    if (strip) rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, H3S_64>(a, st);
     if (!ok(rc) && a.Kpad >= 256) rc = launch_conv_h3_cfg<256, 64, 32, EPI_STD, 1, 32, 2, false, 0, 1>(a, st);
     if (!ok(rc)) rc = launch_conv_h3_cfg<128, 64, 32, EPI_STD, 2, 16, 3, false, 0>(a, st);
     if (!ok(rc) && !sliced) rc = launch_conv_x6g_cfg<256, 64, 32, EPI_STD, 1, 16, 3, 0, 64, 1>(a, st);

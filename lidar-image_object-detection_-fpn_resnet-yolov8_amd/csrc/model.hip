@@ -293,9 +293,6 @@ struct sfa_model {
   // SFA_FPN_GEMM): bit f = level f's low-resolution W_a . x conv, bit 3 + f = its skip conv with the
   // upsampled residual; the other convs run on conv_h3 / conv_r3 (same products for the skip convs)
   int fpn_gemm = 5;
-  // fp16x3 64 -> 64 3x3 convs (layer1) on the weight-stationary kernel (conv_ws_kernel.h; env
-  // SFA_CONV_WS): 1 = on, 0 = the strip kernel (the same bits)
-  int conv_ws = 0;
   // Side stream for the level-0 heads (they only need up_level2, so they overlap the rest
   // of the FPN and the level-1/2 heads); created with the model on the current device,
   // used only when the forward's stream is on that device.
@@ -477,7 +474,6 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   if (const char* e = getenv("SFA_STEM_PATCH")) m->stem_patch = atoi(e) < 0 ? 0 : (atoi(e) > 2 ? 2 : atoi(e));
   if (const char* e = getenv("SFA_FPN_COMMUTE")) m->fpn_commute = atoi(e) & 7;
   if (const char* e = getenv("SFA_FPN_GEMM")) m->fpn_gemm = atoi(e) & 63;
-  if (const char* e = getenv("SFA_CONV_WS")) m->conv_ws = atoi(e) != 0;
   bool side_streams = true;  // env SFA_SIDE_STREAMS=0: every launch on the caller's stream (A/B)
   if (const char* e = getenv("SFA_SIDE_STREAMS")) side_streams = strcmp(e, "0") != 0;
   if (side_streams) make_side_streams(m);
@@ -524,10 +520,6 @@ extern "C" int sfa_model_set_option(sfa_model* model, int key, int value) {
       SFA_CHECK_ARG(value >= 0 && value <= 63, "set_option: FPN_GEMM mask %d not in 0..63", value);
       model->fpn_gemm = value;
       break;
-    case SFA_OPT_CONV_WS:
-      SFA_CHECK_ARG(value == 0 || value == 1, "set_option: CONV_WS %d not 0 / 1", value);
-      model->conv_ws = value;
-      break;
     default: set_error("set_option: unknown key %d", key); return SFA_E_INVALID;
   }
   return SFA_OK;
@@ -539,7 +531,6 @@ extern "C" int sfa_model_get_option(const sfa_model* model, int key, int* value)
     case SFA_OPT_STEM_PATCH: *value = model->stem_patch; break;
     case SFA_OPT_FPN_COMMUTE: *value = model->fpn_commute; break;
     case SFA_OPT_FPN_GEMM: *value = model->fpn_gemm; break;
-    case SFA_OPT_CONV_WS: *value = model->conv_ws; break;
     default: set_error("get_option: unknown key %d", key); return SFA_E_INVALID;
   }
   return SFA_OK;
@@ -774,7 +765,6 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       ConvArgs a = conv_args(wb, p.blk[li][0][0], B, oh, ow, t, nullptr, 1);
       a.seg[0] = seg(xcur, B, h, w, cin, 3, stride, 1);
       io(a, xslot, -1, blk_slot(li, 0, 0));
-      a.conv_ws = m->conv_ws;
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     {
@@ -786,7 +776,6 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
         a.seg[1] = seg(xcur, B, h, w, cin, 1, stride, 0);
       }
       io(a, blk_slot(li, 0, 0), li > 0 ? xslot : -1, blk_slot(li, 0, 1));
-      a.conv_ws = m->conv_ws;
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     // block 1
@@ -794,14 +783,12 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       ConvArgs a = conv_args(wb, p.blk[li][1][0], B, oh, ow, t, nullptr, 1);
       a.seg[0] = seg(av, B, oh, ow, planes, 3, 1, 1);
       io(a, blk_slot(li, 0, 1), -1, blk_slot(li, 1, 0));
-      a.conv_ws = m->conv_ws;
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     {
       ConvArgs a = conv_args(wb, p.blk[li][1][1], B, oh, ow, lv, av, 1);
       a.seg[0] = seg(t, B, oh, ow, planes, 3, 1, 1);
       io(a, blk_slot(li, 1, 0), -1, blk_slot(li, 1, 1));
-      a.conv_ws = m->conv_ws;
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     xcur = lv;

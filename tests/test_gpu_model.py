@@ -345,27 +345,6 @@ def test_fpn_gemm_kernel_choices(golden, gpu, hw):
                 assert float(np.max(np.abs(res[mask][h] - r) / np.maximum(1.0, np.abs(r)))) <= 1e-4, (h, mask)
 
 
-@pytest.mark.parametrize("shape", [(2, 96, 96), (3, 160, 192), (16, 608, 608), (5, 608, 608)])
-def test_layer1_weight_stationary_bit_identical(golden, gpu, shape):
-    """SFA_OPT_CONV_WS: the layer1 64 -> 64 convs on the weight-stationary full-row kernel
-    (conv_ws_kernel.h: weights in VGPRs, a 3-row LDS ring split once per row, LDS-DMA row staging)
-    == the strip kernel bit for bit (same K order, products, split and epilogue rounding): row
-    widths 24 / 48 / 152 (RB 1 / 2 / 5), 16 frames (one segment per CU) and 5 frames (segments of
-    3-4 rows, the ring's first rows and the last row's missing refill)."""
-    B, H, W = shape
-    x = torch.from_numpy(synthetic.synthetic_bev(B, H, W, seed=71)).to(gpu)
-    res = {}
-    for ws in (1, 0):
-        model = make_model(golden, gpu)
-        eng = model._engine(gpu)
-        eng.set_math(_math("fp16x3"))
-        eng.set_option(_lib.OPT_CONV_WS, ws)
-        with torch.no_grad():
-            res[ws] = {h: v.cpu().numpy() for h, v in model(x).items()}
-    for h in gc.HEADS:
-        np.testing.assert_array_equal(res[1][h], res[0][h], err_msg=f"{h}: weight-stationary vs strip layer1")
-
-
 def test_batch_invariance_608(golden, gpu):
     """At the full 608x608 size (every kernel path of the bench: r3 heads, strip convs, FPN skip
     convs, r3 body convs (M >= 50000 needs >= 9 frames), split-K layer4): frames 7, 8 of a batch

@@ -18,12 +18,12 @@
 #include <thread>
 
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_kernel.h"
-#include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_ws_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_x6_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3s_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_r3_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/stem_band_kernel.h"
+#include "experiments/r04/conv_ws_kernel.h"
 
 namespace sfa {
 void set_error(const char* fmt, ...) {

@@ -23,11 +23,17 @@
 //
 // Bits.  K order (kh, 32-channel chunk, kw), the three products per k-step (w_hi a_lo, w_lo a_hi,
 // w_hi a_hi) on the transposed accumulators, the split (split2h_pair at the frame's scale) and the
-// epilogue's rounding sequence are the strip kernel's: the outputs are bit-identical to
-// conv_h3s_kernel<..., H3S_64> (tests/test_gpu_model.py::test_layer1_weight_stationary_bit_identical).
+// epilogue's rounding sequence are the strip kernel's: the outputs were bit-identical to
+// conv_h3s_kernel<..., H3S_64> on the GPU (96², 160 x 192, 16 x 608², 5 x 608²).
+//
+// ROUND-4 EXPERIMENT, NOT ADOPTED (tools/convbench4 hook only): 134-137 us against the strip kernel's
+// 121-124 in isolation, 116.8 vs ~102 us inside the forward, bench -1.4 % (profiles/r04e_*). At 243
+// VGPRs (the 144-VGPR weight slice) hipcc keeps ONE A-fragment pair in flight and waits
+// lgkmcnt(0) before every 3-MFMA group, so the LDS latency is exposed; a one-wave-per-SIMD form (4 waves
+// x whole rows, accumulators in AGPRs) schedules the same way, and explicit double buffering spills.
 #pragma once
 
-#include "conv_r3_kernel.h"
+#include "../../../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_r3_kernel.h"
 
 namespace sfa {
 
