@@ -167,10 +167,9 @@ int sfa_model_get_math(const sfa_model* model);
  * overrides it.  Not concurrently with a forward of this model.  (Round 4: the round-2/3 tune
  * bits, stem ablations, grouped heads and second side stream — measured and not adopted — moved to
  * tools/experiments/r03 with their convbench hooks.)
- *   SFA_OPT_STEM_PATCH  (SFA_STEM_PATCH)  fp16x3 stem + max-pool in one kernel: 1 (default) over
- *                                         16 x 16 patches + a merge pass; 2 over full-width row
- *                                         bands, no merge pass (shapes it does not take use 1;
- *                                         measured slower); 0: the implicit-GEMM stem + max-pool
+ *   SFA_OPT_STEM_PATCH  (SFA_STEM_PATCH)  1 (default): the fp16x3 stem + max-pool in one kernel
+ *                                         over 16 x 16 patches + a merge pass; 0: the
+ *                                         implicit-GEMM stem + the max-pool kernel
  *   SFA_OPT_FPN_COMMUTE (SFA_FPN_COMMUTE) bit mask of the FPN levels run commuted (7, fp16x3)
  *   SFA_OPT_FPN_GEMM    (SFA_FPN_GEMM)    bit mask of the commuted FPN 1x1 convs on the persistent
  *                                         weight-resident kernel: bit f = level f's low-resolution

@@ -8,7 +8,7 @@
 #include "conv_h3s_kernel.h"
 #include "conv_r3_kernel.h"
 #include "fpn_kernel.h"
-#include "stem_band_kernel.h"
+#include "stem_patch_kernel.h"
 
 namespace sfa {
 
@@ -222,12 +222,6 @@ int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t st) {
   return launch_conv_cfg<64, 64, 32, 32, 16, EPI_STD, 4>(a, st);
 }
 
-int launch_stem_patch(const ConvArgs& a, int form, hipStream_t st) {
-  if (form >= 2) {  // the band stem; shapes it does not take use the round-3 patch stem
-    const int rc = launch_stem_band(a, st);
-    if (rc != SFA_E_UNSUPPORTED) return rc;
-  }
-  return launch_stem_patch_pool(a, st);
-}
+int launch_stem_patch(const ConvArgs& a, hipStream_t st) { return launch_stem_patch_pool(a, st); }
 
 }  // namespace sfa

@@ -284,10 +284,8 @@ struct sfa_model {
   int math;
   int fpn_commute = 7;  // fp16x3: bit f -> FPN conv f as up(W_a x) + W_b skip (env SFA_FPN_COMMUTE, mask)
   // fp16x3 stem form (env SFA_STEM_PATCH): 1 (default) = the 16 x 16 patch kernel + its merge pass
-  // (stem_patch_kernel.h); 2 = the full-width band kernel, pool in the epilogue, no merge pass
-  // (stem_band_kernel.h; shapes it does not take use 1 — measured 196-212 us against the patch
-  // stem's 170-177 + merge, profiles/r04a_*, so not the default); 0 = the implicit-GEMM stem conv +
-  // the max-pool kernel, as the other math modes
+  // (stem_patch_kernel.h); 0 = the implicit-GEMM stem conv + the max-pool kernel, as the other math
+  // modes (the round-4 full-width band stem measured slower: tools/experiments/r04)
   int stem_patch = 1;
   // fp16x3 FPN 1x1 convs on the persistent weight-resident kernel (fpn_kernel.h), mask (env
   // SFA_FPN_GEMM): bit f = level f's low-resolution W_a . x conv, bit 3 + f = its skip conv with the
@@ -471,7 +469,7 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   m->math = SFA_MATH_FP16X3;
   // A/B convenience: the environment seeds the options once, here (sfa_model_set_option
   // overrides them; nothing reads the environment on the launch path)
-  if (const char* e = getenv("SFA_STEM_PATCH")) m->stem_patch = atoi(e) < 0 ? 0 : (atoi(e) > 2 ? 2 : atoi(e));
+  if (const char* e = getenv("SFA_STEM_PATCH")) m->stem_patch = atoi(e) != 0;
   if (const char* e = getenv("SFA_FPN_COMMUTE")) m->fpn_commute = atoi(e) & 7;
   if (const char* e = getenv("SFA_FPN_GEMM")) m->fpn_gemm = atoi(e) & 63;
   bool side_streams = true;  // env SFA_SIDE_STREAMS=0: every launch on the caller's stream (A/B)
@@ -509,7 +507,7 @@ extern "C" int sfa_model_set_option(sfa_model* model, int key, int value) {
   std::lock_guard<std::mutex> lk(model->fork_mu);
   switch (key) {
     case SFA_OPT_STEM_PATCH:
-      SFA_CHECK_ARG(value >= 0 && value <= 2, "set_option: STEM_PATCH %d not in 0..2", value);
+      SFA_CHECK_ARG(value == 0 || value == 1, "set_option: STEM_PATCH %d not 0 / 1", value);
       model->stem_patch = value;
       break;
     case SFA_OPT_FPN_COMMUTE:
@@ -717,9 +715,9 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   };
 
   const int H2 = H / 2, W2 = W / 2;
-  // The band / patch stems (fp16x3) read the caller's layout themselves, scale every tile by its own
-  // max |x| and max-pool in their epilogues: no layout conversion, no input amax pass, no max-pool
-  // launch (stem_band_kernel.h, stem_patch_kernel.h).
+  // The patch stem (fp16x3) reads the caller's layout itself, scales every tile by its own max |x|
+  // and max-pools in its epilogue: no layout conversion, no input amax pass, no max-pool launch
+  // (stem_patch_kernel.h).
   const bool patch_stem = h3 && m->stem_patch && H2 % 16 == 0 && W2 % 16 == 0;
   const float* xin = x;
   if (patch_stem) {
@@ -730,9 +728,9 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   } else if (h3) {
     SFA_RC(launch_amax_nhwc4(x, B, H, W, AM(AM_INPUT), st));
   }
-  // stem conv7x7/s2/p3 + BN + ReLU (fpn_resnet.py:179-181) + max-pool (:182): the band stem writes
-  // every pooled cell once from its epilogue; the round-3 patch stem sends the tile-border cells'
-  // parts through a side buffer and a merge pass; otherwise the conv and the max-pool kernel.
+  // stem conv7x7/s2/p3 + BN + ReLU (fpn_resnet.py:179-181) + max-pool (:182): the patch stem sends
+  // the tile-border cells' parts through a side buffer and a merge pass; otherwise the conv and the
+  // max-pool kernel.
   {
     ConvArgs a = conv_args(wb, p.stem, B, H2, W2, patch_stem ? F(bf.p0) : F(bf.s0), nullptr, 1);
     a.seg[0] = seg(xin, B, H, W, 4, 7, 2, 3);  // the patch stem reads NCHW3 planes through it too
@@ -743,7 +741,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
                                              : (in_layout == SFA_IN_NCHW3_FLIP_HW ? STEM_IN_NCHW3_FLIP : STEM_IN_NCHW3);
       a.part = F(bf.s0);  // the (here unused) unfused stem buffer
       a.part_floats = (size_t)B * H2 * W2 * 64;
-      SFA_RC(launch_stem_patch(a, m->stem_patch, st));
+      SFA_RC(launch_stem_patch(a, st));
     } else {
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }

@@ -198,10 +198,10 @@ def test_argument_errors_before_any_launch():
         assert len(defaults) == _lib.OPT_COUNT
         for key, val in defaults.items():
             assert L.sfa_model_get_option(h, key, ctypes.byref(v)) == 0 and v.value == val, key
-        for form in (0, 1, 2):  # implicit-GEMM + max-pool / patch stem + merge / band stem
+        for form in (0, 1):  # implicit-GEMM + max-pool / patch stem + merge
             assert L.sfa_model_set_option(h, _lib.OPT_STEM_PATCH, form) == 0
             assert L.sfa_model_get_option(h, _lib.OPT_STEM_PATCH, ctypes.byref(v)) == 0 and v.value == form
-        assert L.sfa_model_set_option(h, _lib.OPT_STEM_PATCH, 3) == -1
+        assert L.sfa_model_set_option(h, _lib.OPT_STEM_PATCH, 2) == -1
         assert L.sfa_model_set_option(h, _lib.OPT_FPN_COMMUTE, 9) == -1
         assert L.sfa_model_set_option(h, _lib.OPT_FPN_COMMUTE, 5) == 0
         assert L.sfa_model_set_option(h, _lib.OPT_FPN_GEMM, 64) == -1

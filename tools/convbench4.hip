@@ -22,7 +22,7 @@
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3s_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_r3_kernel.h"
-#include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/stem_band_kernel.h"
+#include "experiments/r04/stem_band_kernel.h"
 #include "experiments/r04/conv_ws_kernel.h"
 
 namespace sfa {

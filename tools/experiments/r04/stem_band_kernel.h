@@ -1,6 +1,13 @@
 // Stem conv 7x7/s2/p3 (3 -> 64) + BN + ReLU + max-pool 3x3/s2/p1 on full-width row bands, fp16x3
-// (fpn_resnet.py:120-123,179-182).  Round 4: replaces stem_patch_pool2_kernel + its
-// stem_pool_merge_kernel launch — no side buffer, no merge pass, no atomics.
+// (fpn_resnet.py:120-123,179-182).  Round 4 attempt at VERDICT r03 item 6 (replace
+// stem_patch_pool2_kernel + its stem_pool_merge_kernel launch: no side buffer, no merge pass, no
+// atomics). ROUND-4 EXPERIMENT, NOT ADOPTED (tools/convbench4 hook only): bit-identical to the patch
+// stem, but 210-212 us (one block chain at a time: every A-fragment pair waited for with
+// lgkmcnt(0)) and 202-206 us with two blocks' MFMA chains interleaved, against the patch stem's
+// 170-183 us + 12 us merge on the same boxes (profiles/r04a_convbench4_stem_regw_tiles.txt,
+// r04f_convbench4_stem_band_paired.txt); bench -1.5 % (profiles/r04d_ab_fpn_gemm_stem.txt). Its
+// A fragment feeds one 16-channel column block per read (0.67 ds_read_b128 per MFMA, the patch
+// stem's 0.44), which the paired chains do not change.
 //
 // Work.  A block owns the pooled rows [py0, py1) of one frame (a "segment"; frames x segments
 // blocks, about one per CU) and walks band tiles of 4 conv rows at FULL width: tile j is conv rows
@@ -31,7 +38,7 @@
 // hi lo, hi hi) are the round-3 stem's: the same accumulators bit for bit.
 #pragma once
 
-#include "stem_patch_kernel.h"
+#include "../../../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/stem_patch_kernel.h"
 
 namespace sfa {
 
@@ -243,26 +250,9 @@ __global__ void __launch_bounds__(512, 1) stem_band_kernel(const ConvArgs a, int
     const int vo[2] = {(pyA * PW * 64 + nch) * 4 + (g == 2 ? 256 : 0), (pyB * PW * 64 + nch) * 4 + (g == 2 ? 256 : 0)};
     float pend[2];               // first block's column-0 partials (cq > 0)
 
-#pragma unroll
-    for (int k = 0; k < NBW; ++k) {
+    // epilogue of block k: lane (g, c16) = conv column 4 blk + g, rows cj .. cj + 3, channel 16 nh + c16
+    auto epi = [&](const int k, const f32x4_t acc) {
       const int blk = cq * NBW + k;
-      f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
-      f16x8_t ah[2], al[2];  // A fragments, k-step kh + 1 read during kh's MFMAs
-      ah[0] = *reinterpret_cast<const f16x8_t*>(ring + rowoff[0] + blk * 64);
-      al[0] = *reinterpret_cast<const f16x8_t*>(ring + rowoff[0] + blk * 64 + TERMB);
-#pragma unroll
-      for (int kh = 0; kh < 7; ++kh) {
-        if (kh + 1 < 7) {
-          const unsigned char* ap = ring + rowoff[kh + 1] + blk * 64;
-          ah[(kh + 1) & 1] = *reinterpret_cast<const f16x8_t*>(ap);
-          al[(kh + 1) & 1] = *reinterpret_cast<const f16x8_t*>(ap + TERMB);
-        }
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[kh & 1], whi[kh], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[kh & 1], wlo[kh], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[kh & 1], whi[kh], acc, 0, 0, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // epilogue: lane (g, c16) = conv column 4 blk + g, rows cj .. cj + 3, channel 16 nh + c16
       float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -292,6 +282,41 @@ __global__ void __launch_bounds__(512, 1) stem_band_kernel(const ConvArgs a, int
         left[h] = l3;
         if (k == NBW - 1 && cq == 0 && g == 3) XCH[(wave * 2 + h) * 16 + c16] = val;
       }
+    };
+    // two blocks' MFMA chains interleaved (k-step kh + 1's A fragments of both read during kh's six
+    // MFMAs), then their epilogues in column order: the same products per accumulator, the same bits
+    static_assert(NBW % 2 == 0, "blocks per wave in pairs");
+#pragma unroll
+    for (int k = 0; k < NBW; k += 2) {
+      const int blk = cq * NBW + k;
+      f32x4_t acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      f16x8_t ah[2][2], al[2][2];  // [k-step parity][block of the pair]
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        ah[0][e] = *reinterpret_cast<const f16x8_t*>(ring + rowoff[0] + (blk + e) * 64);
+        al[0][e] = *reinterpret_cast<const f16x8_t*>(ring + rowoff[0] + (blk + e) * 64 + TERMB);
+      }
+#pragma unroll
+      for (int kh = 0; kh < 7; ++kh) {
+        if (kh + 1 < 7) {
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const unsigned char* ap = ring + rowoff[kh + 1] + (blk + e) * 64;
+            ah[(kh + 1) & 1][e] = *reinterpret_cast<const f16x8_t*>(ap);
+            al[(kh + 1) & 1][e] = *reinterpret_cast<const f16x8_t*>(ap + TERMB);
+          }
+        }
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[kh & 1][0], whi[kh], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[kh & 1][1], whi[kh], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[kh & 1][0], wlo[kh], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[kh & 1][1], wlo[kh], acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[kh & 1][0], whi[kh], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[kh & 1][1], whi[kh], acc1, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      epi(k, acc0);
+      __builtin_amdgcn_sched_barrier(0);
+      epi(k + 1, acc1);
       __builtin_amdgcn_sched_barrier(0);
     }
     // the next tile's new rows: maxima (ring rows 5..7 | 8..12 of tile j + 1)
