@@ -14,7 +14,7 @@ for r in csv.DictReader(open(os.path.join(base, "p1", "run_counter_collection.cs
                             "us": (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3})
     e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
 rows = list(rows.values())
-starts = [i for i, r in enumerate(rows) if "nchw3_to_nhwc4" in r["name"]]
+starts = [i for i, r in enumerate(rows) if "nchw3_to_nhwc4" in r["name"] or "stem_patch" in r["name"]]
 s = starts[-1]
 e = next(i for i in range(s, len(rows)) if "kfpn_combine" in rows[i]["name"])
 tot = collections.Counter()
