@@ -142,6 +142,16 @@ static const size_t g_part_floats = 64u << 20;
           return launch_conv_h3s_cfg<BM, BN, WM, EPI, OCC, ABL>(b, s);                            \
         }                                                                                         \
   }
+#define CANDH3(BM, BN, WM, OCC, NK, NST, KS)                                                        \
+  Cand {                                                                                          \
+    "h3 " #BM "x" #BN " w" #WM " occ" #OCC " ks" #KS, 32, [](const ConvArgs& a, hipStream_t s) {   \
+      ConvArgs b = a;                                                                             \
+      b.ksplit = KS;                                                                              \
+      b.part = g_part;                                                                            \
+      b.part_floats = g_part_floats;                                                              \
+      return launch_conv_h3_cfg<BM, BN, WM, EPI_STD, OCC, NK, NST, false, 2, 1>(b, s);             \
+    }                                                                                             \
+  }
 // the fp16x3 stems (NCHW3 input planes, pooled output): band kernel / round-3 patch kernel + merge
 #define CANDSTEM(FORM)                                                                            \
   Cand {                                                                                          \
@@ -177,6 +187,7 @@ int main(int argc, char** argv) {
       {"layer4 3x3 512->512", 16, 19, 19, 512, 3, 1, 1, 512, false, false},
       {"s2 layer2.0.conv1 3x3/2 64->128", 16, 152, 152, 64, 3, 2, 1, 128, false, false},
       {"s2 layer3.0.conv1 3x3/2 128->256", 16, 76, 76, 128, 3, 2, 1, 256, false, false},
+      {"s2 layer4.0.conv1 3x3/2 256->512", 16, 38, 38, 256, 3, 2, 1, 512, false, false},
       {"head L1 3x3 128->5x64", 16, 152, 152, 128, 3, 1, 1, 320, true, false},
       {"head L2 3x3 64->5x64", 16, 152, 152, 64, 3, 1, 1, 320, true, false},
       {"head L0 3x3 256->5x64", 16, 76, 76, 256, 3, 1, 1, 320, true, false},
@@ -201,6 +212,13 @@ int main(int argc, char** argv) {
       // round 4: grids that fill the chip without split-K (no reduce launch)
       CANDTK(64, 128, 16, EPI_STD, 3, 10, 1), CANDTK(128, 64, 32, EPI_STD, 3, 10, 1),
       CANDTK(128, 64, 32, EPI_STD, 3, 142, 1),
+  };
+  // stride-2 conv1 of layers 2/3 (and 4): the product picks conv_r3 128 x 128 for the big-M layer2 and
+  // conv_h3 128 x 128 for the others (conv.hip); both, and 64-row conv_r3 tiles, on each shape
+  std::vector<Cand> s2 = {
+      CANDR(128, 128, 32, EPI_STD, 2, 2, 526592, 1), CANDH3(128, 128, 32, 2, 32, 2, 1),
+      CANDR(64, 128, 16, EPI_STD, 3, 2, 526592, 1), CANDR(64, 128, 32, EPI_STD, 4, 2, 526592, 1),
+      CANDR(128, 128, 32, EPI_STD, 2, 2, 526592, 1), CANDH3(128, 128, 32, 2, 32, 2, 1),
   };
   std::vector<Cand> heads = {
       CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1),
@@ -274,7 +292,7 @@ int main(int argc, char** argv) {
       off += a.hch[j];
     }
     const double flop = 2.0 * M * sh.N * (double)K;
-    std::vector<Cand>& cands = sh.head ? heads : sh.C == 4 ? stem : (sh.N == 64 ? n64 : sh.N == 512 ? n512 : nbig);
+    std::vector<Cand>& cands = sh.head ? heads : sh.C == 4 ? stem : sh.stride == 2 ? s2 : (sh.N == 64 ? n64 : sh.N == 512 ? n512 : nbig);
     printf("\n== %s  M=%d N=%d K=%d  (%.2f GFLOP)\n", sh.name, M, sh.N, K, flop / 1e9);
     std::vector<float> ref, got;
     ref.clear();
