@@ -173,8 +173,9 @@ int sfa_model_get_math(const sfa_model* model);
  *   SFA_OPT_FPN_COMMUTE (SFA_FPN_COMMUTE) bit mask of the FPN levels run commuted (7, fp16x3)
  *   SFA_OPT_FPN_GEMM    (SFA_FPN_GEMM)    bit mask of the commuted FPN 1x1 convs on the persistent
  *                                         weight-resident kernel: bit f = level f's low-resolution
- *                                         conv, bit 3 + f = its skip conv (5: the low-res convs of
- *                                         levels 0 and 2); the others on the per-tile kernels
+ *                                         conv, bit 3 + f = its skip conv (37: the low-res convs of
+ *                                         levels 0 and 2, the level-2 skip conv on full rows); the
+ *                                         others on the per-tile kernels
  */
 enum sfa_model_option { SFA_OPT_STEM_PATCH = 0, SFA_OPT_FPN_COMMUTE = 1, SFA_OPT_FPN_GEMM = 2 };
 int sfa_model_set_option(sfa_model* model, int key, int value);

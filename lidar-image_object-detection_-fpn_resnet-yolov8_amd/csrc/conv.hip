@@ -94,6 +94,10 @@ constexpr int H3S_128 = 2 | 8;
 static int launch_fpn(const ConvArgs& a, hipStream_t st) {
   const int C = a.seg[0].C;
   if (a.res_up) {
+    if (C == 64 && a.N == 64) {  // the 152-wide level: full rows, taps from an LDS ring
+      const int rc = launch_fpn_row(a, st);
+      if (rc != SFA_E_UNSUPPORTED) return rc;
+    }
     if (C == 64 && a.N % 64 == 0) return launch_fpn_gemm_cfg<64, 64, true, 3>(a, st);
     if (C == 128 && a.N % 128 == 0) return launch_fpn_gemm_cfg<128, 128, true, 2>(a, st);
     if (C == 256 && a.N % 128 == 0) return launch_fpn_gemm_cfg<256, 128, true, 1>(a, st);

@@ -260,4 +260,229 @@ inline int launch_fpn_gemm_cfg(const ConvArgs& a, hipStream_t st) {
   return SFA_OK;
 }
 
+
+// FPN skip conv of the 152-wide level (up_level4 = W_b . layer1 + b + up2x(W_a . c2): K = N = 64) on
+// full output rows (round 4).  The per-tile kernels (conv_r3 R3_FPN, fpn_gemm above) gather the
+// epilogue's four bilinear taps from L2 just before use — 16 float4 loads per lane per 32-row tile,
+// their latency exposed (PMC: waves waiting 70 % of their cycles, 3.1 TB/s).  Here a block walks
+// the rows of one frame segment; the half-resolution source rows the bilinear taps need live in an
+// LDS ring of 3 rows (each loaded ONCE per segment by LDS-DMA, one row ahead: output row y needs
+// source rows y0(y), y0(y) + 1 and y0 advances by at most one per output row), the weight slice in
+// LDS, the next row's A fragments prefetched into VGPRs during this row's epilogue.  Products, K
+// order, split and the epilogue's rounding sequence are conv_r3_kernel's (R3_FPN): the same bits.
+namespace fpn_row {
+constexpr int NT = 256, NW = 4, K = 64, N = 64, KT = K / 32, TNB = N / 16;
+constexpr int BROW = 64, TERM_B = N * BROW, STAGE = 2 * TERM_B, W_BYTES = KT * STAGE;  // 16 KiB
+__host__ __device__ constexpr int slot_bytes(int RB) { return 8 * RB * N * 4; }  // half-width source row
+__host__ __device__ constexpr int lds_bytes(int RB) { return W_BYTES + 3 * slot_bytes(RB) + 2 * N * 4 + NW * 4; }
+}  // namespace fpn_row
+
+template <int RB>  // 16-pixel row blocks per output row: W <= 16 RB
+__global__ void __launch_bounds__(256, 2) fpn_row_kernel(const ConvArgs a, int segs) {
+#pragma clang fp contract(off)
+  using namespace fpn_row;
+  constexpr int RBW = (RB + NW - 1) / NW;  // row blocks per wave (wave w: w, w + NW, ..)
+  constexpr int SLOT = slot_bytes(RB);
+  __shared__ __attribute__((aligned(16))) unsigned char smem[lds_bytes(RB)];
+  unsigned char* const ring = smem + W_BYTES;
+  float* const CSB = reinterpret_cast<float*>(smem + W_BYTES + 3 * SLOT);  // [N] winv, [N] bias
+  float* const red = CSB + 2 * N;
+  auto swzB = [](int R) { return ((R >> 2) & 3) ^ ((((R & 15) + 4) >> 3) & 1); };
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c16 = lane & 15, g = lane >> 4;
+  const int H = a.OH, W = a.OW, Hh = H >> 1, Wh = W >> 1;
+  const int b = blockIdx.x / segs, sk = blockIdx.x - b * segs;
+  const int y0 = sk * H / segs, y1 = (sk + 1) * H / segs;
+  if (y1 <= y0) return;  // uniform per block
+
+  // the weight slice (K columns from wk0) in conv_r3's swizzled fragment layout
+  {
+    const int wst = a.wstride ? a.wstride : a.Kpad;
+    const size_t term_elems = (size_t)a.N * wst;
+    for (int c = tid; c < KT * 2 * N * 4; c += NT) {
+      const int q = c & 3, n = (c >> 2) % N, rest = (c >> 2) / N, term = rest & 1, kt = rest >> 1;
+      const r3_u32x4 v = *reinterpret_cast<const r3_u32x4*>(a.wh + term * term_elems + (size_t)n * wst + a.wk0 + kt * 32 + 8 * q);
+      *reinterpret_cast<r3_u32x4*>(smem + kt * STAGE + term * TERM_B + n * BROW + ((q ^ swzB(n)) << 4)) = v;
+    }
+  }
+  for (int i = tid; i < N; i += NT) {
+    CSB[i] = a.winv[i];
+    CSB[N + i] = a.bias ? a.bias[i] : 0.f;
+  }
+  float ainv;
+  const float as = amax_frame_scale(a.amax_in, 1, b, ainv);
+  ainv = 1.f / as;  // as conv_r3 forms it
+
+  // source rows (half resolution, pixel-major, N channels) by LDS-DMA: 1 KiB pieces
+  const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.res_up), (short)0, (int)((size_t)(a.M / (H * W)) * Hh * Wh * N * 4), 0x00020000);
+  const int src_bytes = Wh * N * 4;
+  auto dma_src = [&](int sy) {
+    unsigned char* dst = ring + (sy % 3) * SLOT;
+    const unsigned rbase = (unsigned)(((size_t)(b * Hh + sy) * Wh) * N * 4);
+    for (int piece = wave; piece * 1024 < src_bytes; piece += NW) {
+      const unsigned off = piece * 1024 + lane * 16 < src_bytes ? rbase + piece * 1024 + lane * 16 : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsr, (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16,
+                                               off, 0, 0, 0);
+    }
+  };
+  auto srow0 = [&](int y) { return (int)(a.res_sh * (float)y); };
+
+  // A: lane (c16, g) of row block rb -> pixel 16 rb + c16, channels 32 kt + 8 g .. + 7
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.seg[0].x), (short)0,
+                                                                       (int)a.seg[0].bytes, 0x00020000);
+  r3_u32x4 ra[RBW][KT][2];
+  auto load_a = [&](int y) {
+#pragma unroll
+    for (int i = 0; i < RBW; ++i) {
+      const int x = 16 * (wave + NW * i) + c16;
+      const bool ok = wave + NW * i < RB && x < W;
+      const unsigned base = ok ? (unsigned)((((size_t)(b * H + y) * W + x) * K + 8 * g) * 4) : 0x80000000u;
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        const unsigned off = ok ? base + kt * 128u : base;
+        ra[i][kt][0] = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
+        ra[i][kt][1] = __builtin_amdgcn_raw_buffer_load_b128(rsx, off + 16u, 0, 0);
+      }
+    }
+  };
+
+  // prologue: source rows of the first output row, its A fragments
+  int hi_row = min(srow0(y0) + 1, Hh - 1);  // highest source row in the ring
+  for (int sy = srow0(y0); sy <= hi_row; ++sy) dma_src(sy);
+  load_a(y0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int bfo = c16 * BROW + ((g ^ swzB(c16)) << 4);
+  float tmx = 0.f;
+  for (int y = y0; y < y1; ++y) {
+    // the source row the next output row may need beyond the ring's top (its slot held a row <= y0(y) - 1)
+    const int want = min(srow0(y) + 2, Hh - 1);
+    const bool dma = y + 1 < y1 && want > hi_row;
+    if (dma) {
+      dma_src(want);
+      hi_row = want;
+    }
+    // this row's A split into fp16 terms first, so the next row's loads go out before the MFMAs
+    f16x8_t hf[RBW][KT][2];
+#pragma unroll
+    for (int i = 0; i < RBW; ++i)
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+        split2h_x8(__builtin_bit_cast(x6_f32x4, ra[i][kt][0]), __builtin_bit_cast(x6_f32x4, ra[i][kt][1]), as,
+                   hf[i][kt][0], hf[i][kt][1]);
+    if (y + 1 < y1) load_a(y + 1);  // the next row's A flies during this row's MFMAs and epilogue
+    f32x4_t acc[RBW][TNB];
+#pragma unroll
+    for (int i = 0; i < RBW; ++i) {
+#pragma unroll
+      for (int ni = 0; ni < TNB; ++ni) acc[i][ni] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+        const unsigned char* S = smem + kt * STAGE;
+#pragma unroll
+        for (int ni = 0; ni < TNB; ++ni) {
+          const f16x8_t c0 = *reinterpret_cast<const f16x8_t*>(S + bfo + ni * 16 * BROW);
+          const f16x8_t c1 = *reinterpret_cast<const f16x8_t*>(S + TERM_B + bfo + ni * 16 * BROW);
+          f32x4_t cc = acc[i][ni];
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[i][kt][1], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c1, hf[i][kt][0], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[i][kt][0], cc, 0, 0, 0);
+          acc[i][ni] = cc;
+        }
+      }
+    }
+    // epilogue (r3t_epilogue_std with the upsampled residual): taps from the ring
+    const float fy = a.res_sh * (float)y;
+    const int sy0 = (int)fy, sy1 = sy0 + (sy0 < Hh - 1 ? 1 : 0);
+    const float ly1 = fy - (float)sy0, ly0 = 1.f - ly1;
+    const unsigned char* R0 = ring + (sy0 % 3) * SLOT;
+    const unsigned char* R1 = ring + (sy1 % 3) * SLOT;
+#pragma unroll
+    for (int i = 0; i < RBW; ++i) {
+      const int x = 16 * (wave + NW * i) + c16;
+      if (wave + NW * i >= RB) continue;  // wave-uniform
+      const float fx = a.res_sw * (float)x;
+      const int sx0 = (int)fx, sx1 = sx0 + (sx0 < Wh - 1 ? 1 : 0);
+      const float lx1 = fx - (float)sx0, lx0 = 1.f - lx1;
+      const bool in = x < W;
+      const int o0 = (in ? sx0 : 0) * N * 4, o1 = (in ? sx1 : 0) * N * 4;
+#pragma unroll
+      for (int ni = 0; ni < TNB; ++ni) {
+        const int n = ni * 16 + 4 * g;
+        const x6_f32x4 a00 = *reinterpret_cast<const x6_f32x4*>(R0 + o0 + n * 4);
+        const x6_f32x4 a01 = *reinterpret_cast<const x6_f32x4*>(R0 + o1 + n * 4);
+        const x6_f32x4 a10 = *reinterpret_cast<const x6_f32x4*>(R1 + o0 + n * 4);
+        const x6_f32x4 a11 = *reinterpret_cast<const x6_f32x4*>(R1 + o1 + n * 4);
+        const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(CSB + n);
+        const x6_f32x4 bn = *reinterpret_cast<const x6_f32x4*>(CSB + N + n);
+        x6_f32x4 val;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float rv = fmaf(ly0, fmaf(lx0, a00[v], lx1 * a01[v]), ly1 * fmaf(lx0, a10[v], lx1 * a11[v]));
+          float t = fmaf(acc[i][ni][v] * ainv, cs[v], bn[v]);
+          t += rv;
+          if (a.relu) t = fmaxf(t, 0.f);
+          val[v] = t;
+        }
+        if (in) {
+          *reinterpret_cast<x6_f32x4*>(a.y + ((size_t)(b * H + y) * W + x) * N + n) = val;
+          tmx = fmaxf(tmx, fmaxf(fmaxf(fabsf(val[0]), fabsf(val[1])), fmaxf(fabsf(val[2]), fabsf(val[3]))));
+        }
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next row's A and this wave's DMA pieces
+    __syncthreads();  // the ring slot written above is visible; every wave is done with this row's taps
+  }
+  if (a.amax_out) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) tmx = fmaxf(tmx, __shfl_xor(tmx, o, 64));
+    if (lane == 0) red[wave] = tmx;
+    __syncthreads();
+    if (tid == 0) {
+      float m = red[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) m = fmaxf(m, red[w]);
+      if (m > 0.f) amax_atomic(a.amax_out, b, m);
+    }
+  }
+}
+
+// The 64 -> 64 FPN skip conv with an upsampled residual on full output rows, W <= 160 and even
+// output dims (RB = ceil(W / 16) in {3, 5, 10}: the 152-wide level of 608 inputs, 40 / 80 at the
+// test sizes); SFA_E_UNSUPPORTED otherwise.
+inline int launch_fpn_row(const ConvArgs& a, hipStream_t st) {
+  using namespace fpn_row;
+  const ConvSeg& g = a.seg[0];
+  if (a.nseg != 1 || g.KH != 1 || g.KW != 1 || g.stride != 1 || g.pad != 0 || g.C != K || a.Kpad != K || a.N != N ||
+      !a.wh || !a.winv || a.res || !a.res_up || a.ksplit > 1 || a.OH != g.H || a.OW != g.W || a.OH % 2 || a.OW % 2 ||
+      (a.wstride && (a.wstride < a.wk0 + K || a.wk0 % 8 != 0)))
+    return SFA_E_UNSUPPORTED;
+  const int RB = (a.OW + 15) / 16;
+  if (RB != 3 && RB != 5 && RB != 10) return SFA_E_UNSUPPORTED;
+  const int frames = a.M / (a.OH * a.OW);
+  if (frames <= 0) return SFA_OK;
+  if ((size_t)frames * (a.OH / 2) * (a.OW / 2) * N * 4 >= (1ull << 31)) return SFA_E_UNSUPPORTED;
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+      ncu = 256;
+  }
+  int segs = (2 * ncu + frames - 1) / frames;  // about two blocks per CU
+  segs = segs < 1 ? 1 : (segs > a.OH ? a.OH : segs);
+  const dim3 gd((unsigned)(frames * segs)), bd(NT);
+  if (RB == 10)
+    hipLaunchKernelGGL(fpn_row_kernel<10>, gd, bd, 0, st, a, segs);
+  else if (RB == 5)
+    hipLaunchKernelGGL(fpn_row_kernel<5>, gd, bd, 0, st, a, segs);
+  else
+    hipLaunchKernelGGL(fpn_row_kernel<3>, gd, bd, 0, st, a, segs);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
 }  // namespace sfa

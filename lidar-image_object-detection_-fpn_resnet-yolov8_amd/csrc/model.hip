@@ -287,10 +287,12 @@ struct sfa_model {
   // (stem_patch_kernel.h); 0 = the implicit-GEMM stem conv + the max-pool kernel, as the other math
   // modes (the round-4 full-width band stem measured slower: tools/experiments/r04)
   int stem_patch = 1;
-  // fp16x3 FPN 1x1 convs on the persistent weight-resident kernel (fpn_kernel.h), mask (env
-  // SFA_FPN_GEMM): bit f = level f's low-resolution W_a . x conv, bit 3 + f = its skip conv with the
-  // upsampled residual; the other convs run on conv_h3 / conv_r3 (same products for the skip convs)
-  int fpn_gemm = 5;
+  // fp16x3 FPN 1x1 convs on the persistent kernels of fpn_kernel.h, mask (env SFA_FPN_GEMM): bit f =
+  // level f's low-resolution W_a . x conv (weight-resident row streaming), bit 3 + f = its skip conv
+  // with the upsampled residual (level 2: full rows with the taps from an LDS ring); the other convs
+  // run on conv_h3 / conv_r3 (the same products for the skip convs). Default 37 = the low-res convs of
+  // levels 0 and 2 and the level-2 skip conv, the ones measured faster (profiles/r04d_*, r04l_*)
+  int fpn_gemm = 37;
   // Side stream for the level-0 heads (they only need up_level2, so they overlap the rest
   // of the FPN and the level-1/2 heads); created with the model on the current device,
   // used only when the forward's stream is on that device.
