@@ -2,7 +2,7 @@
 # the other BASELINE workloads, serial-heads rocprof (roofline agreement) (GPU box)
 set -u
 export TMPDIR=/tmp
-TAG="${1:-r03f}"
+TAG="${1:-r04z}"
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/t_gpu_$TAG.txt 2>&1 || { echo "pytest failed"; tail -30 gpurun_out/t_gpu_$TAG.txt; exit 1; }
 tail -1 gpurun_out/t_gpu_$TAG.txt
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.txt 2>&1 || { echo "smoke failed"; tail gpurun_out/smoke_$TAG.txt; exit 1; }
