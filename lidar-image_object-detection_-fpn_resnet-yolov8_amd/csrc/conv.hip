@@ -94,7 +94,7 @@ constexpr int H3S_128 = 2 | 8;
 static int launch_fpn(const ConvArgs& a, hipStream_t st) {
   const int C = a.seg[0].C;
   if (a.res_up) {
-    if (C == 64 && a.N == 64) {  // the 152-wide level: full rows, taps from an LDS ring
+    {  // full rows, the bilinear taps from an LDS ring of source rows
       const int rc = launch_fpn_row(a, st);
       if (rc != SFA_E_UNSUPPORTED) return rc;
     }

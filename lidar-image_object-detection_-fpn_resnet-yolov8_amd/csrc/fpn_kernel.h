@@ -261,68 +261,78 @@ inline int launch_fpn_gemm_cfg(const ConvArgs& a, hipStream_t st) {
 }
 
 
-// FPN skip conv of the 152-wide level (up_level4 = W_b . layer1 + b + up2x(W_a . c2): K = N = 64) on
-// full output rows (round 4).  The per-tile kernels (conv_r3 R3_FPN, fpn_gemm above) gather the
-// epilogue's four bilinear taps from L2 just before use — 16 float4 loads per lane per 32-row tile,
-// their latency exposed (PMC: waves waiting 70 % of their cycles, 3.1 TB/s).  Here a block walks
-// the rows of one frame segment; the half-resolution source rows the bilinear taps need live in an
-// LDS ring of 3 rows (each loaded ONCE per segment by LDS-DMA, one row ahead: output row y needs
-// source rows y0(y), y0(y) + 1 and y0 advances by at most one per output row), the weight slice in
-// LDS, the next row's A fragments prefetched into VGPRs during this row's epilogue.  Products, K
+// FPN skip convs (up_level = W_b . skip + b + up2x(W_a . x), the upsampled residual added in the
+// epilogue) on full output rows (round 4).  The per-tile kernels (conv_r3 R3_FPN, fpn_gemm above)
+// gather the epilogue's four bilinear taps from L2 just before use — 16 float4 loads per lane per
+// 32-row tile, their latency exposed (PMC: waves waiting 70 % of their cycles on the 152-wide level,
+// 3.1 TB/s).  Here a block walks the rows of one frame segment for one 64-channel column tile; the
+// half-resolution source rows the taps need live in an LDS ring of 3 rows (each loaded ONCE per
+// segment by LDS-DMA, one row ahead: output row y needs source rows y0(y), y0(y) + 1 and y0 advances
+// by at most one per output row), the weight slice and the channels' scales / biases in LDS, and the
+// next row's A fragments are issued right after this row's split, before its MFMAs.  Products, K
 // order, split and the epilogue's rounding sequence are conv_r3_kernel's (R3_FPN): the same bits.
 namespace fpn_row {
-constexpr int NT = 256, NW = 4, K = 64, N = 64, KT = K / 32, TNB = N / 16;
-constexpr int BROW = 64, TERM_B = N * BROW, STAGE = 2 * TERM_B, W_BYTES = KT * STAGE;  // 16 KiB
-__host__ __device__ constexpr int slot_bytes(int RB) { return 8 * RB * N * 4; }  // half-width source row
-__host__ __device__ constexpr int lds_bytes(int RB) { return W_BYTES + 3 * slot_bytes(RB) + 2 * N * 4 + NW * 4; }
+constexpr int NT = 256, NW = 4, NB = 64, TNB = NB / 16;  // 64 output channels per block
+constexpr int BROW = 64, TERM_B = NB * BROW, STAGE = 2 * TERM_B;
+// RB row blocks of 16 pixels per output row (W <= 16 RB); source rows of W / 2 <= 8 RB pixels
+__host__ __device__ constexpr int slot_bytes(int RB) { return 8 * RB * NB * 4; }
+__host__ __device__ constexpr int lds_bytes(int K, int RB) { return (K / 32) * STAGE + 3 * slot_bytes(RB) + 2 * NB * 4 + NW * 4; }
 }  // namespace fpn_row
 
-template <int RB>  // 16-pixel row blocks per output row: W <= 16 RB
-__global__ void __launch_bounds__(256, 2) fpn_row_kernel(const ConvArgs a, int segs) {
+template <int K, int RB, int OCC>
+__global__ void __launch_bounds__(256, OCC) fpn_row_kernel(const ConvArgs a, int segs) {
 #pragma clang fp contract(off)
   using namespace fpn_row;
+  constexpr int KT = K / 32, W_BYTES = KT * STAGE;
   constexpr int RBW = (RB + NW - 1) / NW;  // row blocks per wave (wave w: w, w + NW, ..)
   constexpr int SLOT = slot_bytes(RB);
-  __shared__ __attribute__((aligned(16))) unsigned char smem[lds_bytes(RB)];
+  static_assert(OCC * lds_bytes(K, RB) <= 160 * 1024, "blocks per CU vs LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[lds_bytes(K, RB)];
   unsigned char* const ring = smem + W_BYTES;
-  float* const CSB = reinterpret_cast<float*>(smem + W_BYTES + 3 * SLOT);  // [N] winv, [N] bias
-  float* const red = CSB + 2 * N;
+  float* const CSB = reinterpret_cast<float*>(smem + W_BYTES + 3 * SLOT);  // [NB] winv, [NB] bias
+  float* const red = CSB + 2 * NB;
   auto swzB = [](int R) { return ((R >> 2) & 3) ^ ((((R & 15) + 4) >> 3) & 1); };
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c16 = lane & 15, g = lane >> 4;
-  const int H = a.OH, W = a.OW, Hh = H >> 1, Wh = W >> 1;
-  const int b = blockIdx.x / segs, sk = blockIdx.x - b * segs;
+  const int H = a.OH, W = a.OW, Hh = H >> 1, Wh = W >> 1, N = a.N;
+  const int nct = N / NB;
+  const int ct = blockIdx.x % nct, rest = blockIdx.x / nct;
+  const int b = rest / segs, sk = rest - b * segs;
+  const int n0 = ct * NB;
   const int y0 = sk * H / segs, y1 = (sk + 1) * H / segs;
   if (y1 <= y0) return;  // uniform per block
 
-  // the weight slice (K columns from wk0) in conv_r3's swizzled fragment layout
+  // the weight slice (columns n0 .., K columns from wk0) in conv_r3's swizzled fragment layout
   {
     const int wst = a.wstride ? a.wstride : a.Kpad;
-    const size_t term_elems = (size_t)a.N * wst;
-    for (int c = tid; c < KT * 2 * N * 4; c += NT) {
-      const int q = c & 3, n = (c >> 2) % N, rest = (c >> 2) / N, term = rest & 1, kt = rest >> 1;
-      const r3_u32x4 v = *reinterpret_cast<const r3_u32x4*>(a.wh + term * term_elems + (size_t)n * wst + a.wk0 + kt * 32 + 8 * q);
+    const size_t term_elems = (size_t)N * wst;
+    for (int c = tid; c < KT * 2 * NB * 4; c += NT) {
+      const int q = c & 3, n = (c >> 2) % NB, r2 = (c >> 2) / NB, term = r2 & 1, kt = r2 >> 1;
+      const r3_u32x4 v = *reinterpret_cast<const r3_u32x4*>(a.wh + term * term_elems + (size_t)(n0 + n) * wst + a.wk0 +
+                                                           kt * 32 + 8 * q);
       *reinterpret_cast<r3_u32x4*>(smem + kt * STAGE + term * TERM_B + n * BROW + ((q ^ swzB(n)) << 4)) = v;
     }
   }
-  for (int i = tid; i < N; i += NT) {
-    CSB[i] = a.winv[i];
-    CSB[N + i] = a.bias ? a.bias[i] : 0.f;
+  for (int i = tid; i < NB; i += NT) {
+    CSB[i] = a.winv[n0 + i];
+    CSB[NB + i] = a.bias ? a.bias[n0 + i] : 0.f;
   }
   float ainv;
   const float as = amax_frame_scale(a.amax_in, 1, b, ainv);
   ainv = 1.f / as;  // as conv_r3 forms it
 
-  // source rows (half resolution, pixel-major, N channels) by LDS-DMA: 1 KiB pieces
+  // source rows (half resolution): the block's NB channels of each pixel, by LDS-DMA (16 B per lane,
+  // LDS in item order = [pixel][NB channels])
   const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(a.res_up), (short)0, (int)((size_t)(a.M / (H * W)) * Hh * Wh * N * 4), 0x00020000);
-  const int src_bytes = Wh * N * 4;
+  const int items = Wh * (NB / 4);
   auto dma_src = [&](int sy) {
     unsigned char* dst = ring + (sy % 3) * SLOT;
-    const unsigned rbase = (unsigned)(((size_t)(b * Hh + sy) * Wh) * N * 4);
-    for (int piece = wave; piece * 1024 < src_bytes; piece += NW) {
-      const unsigned off = piece * 1024 + lane * 16 < src_bytes ? rbase + piece * 1024 + lane * 16 : 0x80000000u;
+    const size_t rbase = ((size_t)(b * Hh + sy) * Wh) * N + n0;  // floats
+    for (int piece = wave; piece * 64 < items; piece += NW) {
+      const int it = piece * 64 + lane;
+      const unsigned off = it < items ? (unsigned)((rbase + (size_t)(it / (NB / 4)) * N + 4 * (it % (NB / 4))) * 4) : 0x80000000u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsr, (__attribute__((address_space(3))) void*)(dst + piece * 1024), 16,
                                                off, 0, 0, 0);
     }
@@ -360,8 +370,7 @@ __global__ void __launch_bounds__(256, 2) fpn_row_kernel(const ConvArgs a, int s
   for (int y = y0; y < y1; ++y) {
     // the source row the next output row may need beyond the ring's top (its slot held a row <= y0(y) - 1)
     const int want = min(srow0(y) + 2, Hh - 1);
-    const bool dma = y + 1 < y1 && want > hi_row;
-    if (dma) {
+    if (y + 1 < y1 && want > hi_row) {
       dma_src(want);
       hi_row = want;
     }
@@ -408,7 +417,7 @@ __global__ void __launch_bounds__(256, 2) fpn_row_kernel(const ConvArgs a, int s
       const int sx0 = (int)fx, sx1 = sx0 + (sx0 < Wh - 1 ? 1 : 0);
       const float lx1 = fx - (float)sx0, lx0 = 1.f - lx1;
       const bool in = x < W;
-      const int o0 = (in ? sx0 : 0) * N * 4, o1 = (in ? sx1 : 0) * N * 4;
+      const int o0 = (in ? sx0 : 0) * NB * 4, o1 = (in ? sx1 : 0) * NB * 4;
 #pragma unroll
       for (int ni = 0; ni < TNB; ++ni) {
         const int n = ni * 16 + 4 * g;
@@ -417,7 +426,7 @@ __global__ void __launch_bounds__(256, 2) fpn_row_kernel(const ConvArgs a, int s
         const x6_f32x4 a10 = *reinterpret_cast<const x6_f32x4*>(R1 + o0 + n * 4);
         const x6_f32x4 a11 = *reinterpret_cast<const x6_f32x4*>(R1 + o1 + n * 4);
         const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(CSB + n);
-        const x6_f32x4 bn = *reinterpret_cast<const x6_f32x4*>(CSB + N + n);
+        const x6_f32x4 bn = *reinterpret_cast<const x6_f32x4*>(CSB + NB + n);
         x6_f32x4 val;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
@@ -428,7 +437,7 @@ __global__ void __launch_bounds__(256, 2) fpn_row_kernel(const ConvArgs a, int s
           val[v] = t;
         }
         if (in) {
-          *reinterpret_cast<x6_f32x4*>(a.y + ((size_t)(b * H + y) * W + x) * N + n) = val;
+          *reinterpret_cast<x6_f32x4*>(a.y + ((size_t)(b * H + y) * W + x) * N + n0 + n) = val;
           tmx = fmaxf(tmx, fmaxf(fmaxf(fabsf(val[0]), fabsf(val[1])), fmaxf(fabsf(val[2]), fabsf(val[3]))));
         }
       }
@@ -450,21 +459,20 @@ __global__ void __launch_bounds__(256, 2) fpn_row_kernel(const ConvArgs a, int s
   }
 }
 
-// The 64 -> 64 FPN skip conv with an upsampled residual on full output rows, W <= 160 and even
-// output dims (RB = ceil(W / 16) in {3, 5, 10}: the 152-wide level of 608 inputs, 40 / 80 at the
-// test sizes); SFA_E_UNSUPPORTED otherwise.
-inline int launch_fpn_row(const ConvArgs& a, hipStream_t st) {
+// An FPN skip conv (1x1, K = C, N a multiple of 64, the upsampled residual) on full output rows: the
+// three KFPN levels' shapes (K 64 / 128 / 256 at widths <= 160 / 80 / 48, even output dims);
+// SFA_E_UNSUPPORTED otherwise.
+template <int K, int RB, int OCC>
+inline int launch_fpn_row_cfg(const ConvArgs& a, hipStream_t st) {
   using namespace fpn_row;
   const ConvSeg& g = a.seg[0];
-  if (a.nseg != 1 || g.KH != 1 || g.KW != 1 || g.stride != 1 || g.pad != 0 || g.C != K || a.Kpad != K || a.N != N ||
-      !a.wh || !a.winv || a.res || !a.res_up || a.ksplit > 1 || a.OH != g.H || a.OW != g.W || a.OH % 2 || a.OW % 2 ||
-      (a.wstride && (a.wstride < a.wk0 + K || a.wk0 % 8 != 0)))
+  if (a.nseg != 1 || g.KH != 1 || g.KW != 1 || g.stride != 1 || g.pad != 0 || g.C != K || a.Kpad != K ||
+      a.N % NB != 0 || !a.wh || !a.winv || a.res || !a.res_up || a.ksplit > 1 || a.OH != g.H || a.OW != g.W ||
+      a.OH % 2 || a.OW % 2 || a.OW > 16 * RB || (a.wstride && (a.wstride < a.wk0 + K || a.wk0 % 8 != 0)))
     return SFA_E_UNSUPPORTED;
-  const int RB = (a.OW + 15) / 16;
-  if (RB != 3 && RB != 5 && RB != 10) return SFA_E_UNSUPPORTED;
   const int frames = a.M / (a.OH * a.OW);
   if (frames <= 0) return SFA_OK;
-  if ((size_t)frames * (a.OH / 2) * (a.OW / 2) * N * 4 >= (1ull << 31)) return SFA_E_UNSUPPORTED;
+  if ((size_t)frames * (a.OH / 2) * (a.OW / 2) * a.N * 4 >= (1ull << 31)) return SFA_E_UNSUPPORTED;
   static int ncu = 0;
   if (ncu == 0) {
     int dev = 0;
@@ -472,17 +480,22 @@ inline int launch_fpn_row(const ConvArgs& a, hipStream_t st) {
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
       ncu = 256;
   }
-  int segs = (2 * ncu + frames - 1) / frames;  // about two blocks per CU
+  const int nct = a.N / NB;
+  int segs = (OCC * ncu + frames * nct - 1) / (frames * nct);  // about OCC blocks per CU
   segs = segs < 1 ? 1 : (segs > a.OH ? a.OH : segs);
-  const dim3 gd((unsigned)(frames * segs)), bd(NT);
-  if (RB == 10)
-    hipLaunchKernelGGL(fpn_row_kernel<10>, gd, bd, 0, st, a, segs);
-  else if (RB == 5)
-    hipLaunchKernelGGL(fpn_row_kernel<5>, gd, bd, 0, st, a, segs);
-  else
-    hipLaunchKernelGGL(fpn_row_kernel<3>, gd, bd, 0, st, a, segs);
+  hipLaunchKernelGGL((fpn_row_kernel<K, RB, OCC>), dim3((unsigned)(frames * segs * nct)), dim3(NT), 0, st, a, segs);
   SFA_LAUNCH_CHECK();
   return SFA_OK;
+}
+
+// the skip conv of each KFPN level by its input channel count (the 608-input widths 152 / 76 / 38 and
+// the test sizes' 48 / 24 / 12 .. 40 / 20 / 10)
+inline int launch_fpn_row(const ConvArgs& a, hipStream_t st) {
+  const int C = a.seg[0].C, W = a.OW;
+  if (C == 64) return W > 80 ? launch_fpn_row_cfg<64, 10, 2>(a, st) : launch_fpn_row_cfg<64, 5, 2>(a, st);
+  if (C == 128) return W > 48 ? launch_fpn_row_cfg<128, 5, 1>(a, st) : launch_fpn_row_cfg<128, 3, 2>(a, st);
+  if (C == 256) return launch_fpn_row_cfg<256, 3, 1>(a, st);
+  return SFA_E_UNSUPPORTED;
 }
 
 }  // namespace sfa
