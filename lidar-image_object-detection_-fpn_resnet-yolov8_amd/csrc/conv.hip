@@ -146,6 +146,11 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
       // chip; same per-element K order, so the same bits (tools/convbench4: 97.7 vs 102.0 us,
       // profiles/r04a_convbench4_stem_regw_tiles.txt)
       rc = launch_conv_h3s_cfg<64, 128, 16, EPI_STD, 3, H3S_128>(b, st);
+    else if (strip && b.ksplit == 2 && a.N == 512 && tile_rows(a) < 50000)
+      // layer4 (184 128 x 128 tiles x 2 slices for 512 block slots): the 64-wide layer1 form, 128 x 64
+      // tiles at 3 blocks / CU (736 blocks for 768 slots); same slices and per-element K order, so the
+      // same bits (tools/convbench4: 102.4-105.0 vs 107.4-110.7 us, profiles/r04o_convbench4_layer4_splits.txt)
+      rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, H3S_64>(b, st);
     else if (strip && (3 * (a.seg[0].C >> 5)) % b.ksplit == 0)
       rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, H3S_128>(b, st);
     else if (!strip && tile_rows(a) >= 50000)  // big-M stride-2 / two-segment: A from registers

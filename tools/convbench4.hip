@@ -212,6 +212,11 @@ int main(int argc, char** argv) {
       // round 4: grids that fill the chip without split-K (no reduce launch)
       CANDTK(64, 128, 16, EPI_STD, 3, 10, 1), CANDTK(128, 64, 32, EPI_STD, 3, 10, 1),
       CANDTK(128, 64, 32, EPI_STD, 3, 142, 1),
+      // round 4 (late): the split-K grids of the other tile shapes (3 blocks / CU) and deeper splits
+      CANDTK(64, 128, 16, EPI_STD, 3, 10, 2), CANDTK(128, 64, 32, EPI_STD, 3, 10, 2),
+      CANDTK(128, 64, 32, EPI_STD, 3, 142, 2), CANDTK(128, 128, 32, EPI_STD, 2, 10, 3),
+      CANDTK(128, 128, 32, EPI_STD, 2, 10, 4), CANDTK(64, 128, 16, EPI_STD, 3, 10, 3),
+      CANDTK(64, 128, 16, EPI_STD, 3, 10, 4), CANDTK(128, 128, 32, EPI_STD, 2, 10, 2),
   };
   // stride-2 conv1 of layers 2/3 (and 4): the product picks conv_r3 128 x 128 for the big-M layer2 and
   // conv_h3 128 x 128 for the others (conv.hip); both, and 64-row conv_r3 tiles, on each shape
@@ -219,6 +224,14 @@ int main(int argc, char** argv) {
       CANDR(128, 128, 32, EPI_STD, 2, 2, 526592, 1), CANDH3(128, 128, 32, 2, 32, 2, 1),
       CANDR(64, 128, 16, EPI_STD, 3, 2, 526592, 1), CANDR(64, 128, 32, EPI_STD, 4, 2, 526592, 1),
       CANDR(128, 128, 32, EPI_STD, 2, 2, 526592, 1), CANDH3(128, 128, 32, 2, 32, 2, 1),
+  };
+  // layer4.0.conv1 (M 5776, N 512): the product's conv_h3 128 x 128 with split-K 2 against other
+  // splits and the 64-row conv_r3 tiles with split-K
+  std::vector<Cand> s2n512 = {
+      CANDH3(128, 128, 32, 2, 32, 2, 2), CANDR(64, 128, 16, EPI_STD, 3, 2, 526592, 2),
+      CANDR(128, 128, 32, EPI_STD, 2, 2, 526592, 2), CANDH3(128, 128, 32, 2, 32, 2, 3),
+      CANDH3(128, 128, 32, 2, 32, 2, 4), CANDR(64, 128, 16, EPI_STD, 3, 2, 526592, 3),
+      CANDR(64, 128, 16, EPI_STD, 3, 2, 526592, 4), CANDH3(128, 128, 32, 2, 32, 2, 2),
   };
   std::vector<Cand> heads = {
       CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1),
@@ -292,7 +305,7 @@ int main(int argc, char** argv) {
       off += a.hch[j];
     }
     const double flop = 2.0 * M * sh.N * (double)K;
-    std::vector<Cand>& cands = sh.head ? heads : sh.C == 4 ? stem : sh.stride == 2 ? s2 : (sh.N == 64 ? n64 : sh.N == 512 ? n512 : nbig);
+    std::vector<Cand>& cands = sh.head ? heads : sh.C == 4 ? stem : sh.stride == 2 ? (sh.N == 512 ? s2n512 : s2) : (sh.N == 64 ? n64 : sh.N == 512 ? n512 : nbig);
     printf("\n== %s  M=%d N=%d K=%d  (%.2f GFLOP)\n", sh.name, M, sh.N, K, flop / 1e9);
     std::vector<float> ref, got;
     ref.clear();
