@@ -205,6 +205,10 @@ int main(int argc, char** argv) {
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 1), CANDTK(128, 128, 32, EPI_STD, 2, 266, 1),
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 1), CANDTK(128, 128, 32, EPI_STD, 2, 266, 1),
       CANDTK(64, 128, 16, EPI_STD, 3, 10, 1), CANDTK(128, 64, 32, EPI_STD, 3, 10, 1),
+      // round 4 (late): split-K grids (layer2: 722 128 x 128 tiles = 1.41 rounds of 512 slots)
+      CANDTK(128, 128, 32, EPI_STD, 2, 10, 2), CANDTK(64, 128, 16, EPI_STD, 3, 10, 2),
+      CANDTK(128, 64, 32, EPI_STD, 3, 142, 2), CANDTK(128, 128, 32, EPI_STD, 2, 10, 4),
+      CANDTK(128, 128, 32, EPI_STD, 2, 10, 1),
   };
   std::vector<Cand> n512 = {
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 2), CANDTK(128, 128, 32, EPI_STD, 2, 266, 2),
