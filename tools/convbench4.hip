@@ -209,6 +209,11 @@ int main(int argc, char** argv) {
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 2), CANDTK(64, 128, 16, EPI_STD, 3, 10, 2),
       CANDTK(128, 64, 32, EPI_STD, 3, 142, 2), CANDTK(128, 128, 32, EPI_STD, 2, 10, 4),
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 1),
+      // round 4 (late): the heads' register-A form with the half-tile stagger and the 3-stage W ring
+      // (R3_HEAD_STAG without the packed head epilogue) on the 3x3/s1 body convs
+      CANDR(128, 128, 32, EPI_STD, 2, 3, 1603844, 1), CANDR(256, 128, 32, EPI_STD, 1, 3, 1603844, 1),
+      CANDR(256, 128, 32, EPI_STD, 2, 3, 1603844, 1), CANDR(128, 128, 32, EPI_STD, 2, 2, 526592, 1),
+      CANDTK(128, 128, 32, EPI_STD, 2, 10, 1),
   };
   std::vector<Cand> n512 = {
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 2), CANDTK(128, 128, 32, EPI_STD, 2, 266, 2),
