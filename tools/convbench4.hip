@@ -22,6 +22,7 @@
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3s_kernel.h"
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_r3_kernel.h"
+#include "experiments/r04/conv_wres_kernel.h"
 #include "experiments/r04/stem_band_kernel.h"
 #include "experiments/r04/conv_ws_kernel.h"
 
@@ -200,6 +201,14 @@ int main(int argc, char** argv) {
   };
   n64.push_back(Cand{"h3 weight-stationary rows", 32, [](const ConvArgs& a, hipStream_t s) { return launch_conv_ws(a, s); }});
   n64.push_back(Cand{"h3 weight-stationary rows", 32, [](const ConvArgs& a, hipStream_t s) { return launch_conv_ws(a, s); }});
+  // round 4 (late): whole weight image resident in LDS, barrier-free register-A waves
+  n64.clear();
+  n64.push_back(CANDTK(128, 64, 32, EPI_STD, 3, 142, 1));
+  n64.push_back(Cand{"h3 wres nw8 pd2", 32, [](const ConvArgs& a, hipStream_t s) { return launch_conv_wres_cfg<64, 8, 2>(a, s); }});
+  n64.push_back(Cand{"h3 wres nw8 pd1", 32, [](const ConvArgs& a, hipStream_t s) { return launch_conv_wres_cfg<64, 8, 1>(a, s); }});
+  n64.push_back(Cand{"h3 wres nw12 pd2", 32, [](const ConvArgs& a, hipStream_t s) { return launch_conv_wres_cfg<64, 12, 2>(a, s); }});
+  n64.push_back(CANDTK(128, 64, 32, EPI_STD, 3, 142, 1));
+  n64.push_back(Cand{"h3 wres nw8 pd2", 32, [](const ConvArgs& a, hipStream_t s) { return launch_conv_wres_cfg<64, 8, 2>(a, s); }});
   std::vector<Cand> stem = {CANDSTEM(1), CANDSTEM(2), CANDSTEM(1), CANDSTEM(2)};
   std::vector<Cand> nbig = {
       CANDTK(128, 128, 32, EPI_STD, 2, 10, 1), CANDTK(128, 128, 32, EPI_STD, 2, 266, 1),
