@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -49,6 +50,22 @@ inline int ilog2(int v) {
   int l = 0;
   while ((1 << l) < v) ++l;
   return l;
+}
+
+// CU count of the device a stream runs on (persistent-grid sizing), cached per device: each slot is
+// written with the device's own answer, so concurrent first calls and launches on several devices
+// agree; 256 (MI355X) when the query fails.
+inline int cu_count(hipStream_t st) {
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cache[kMaxDev];
+  int dev = -1;
+  if (hipStreamGetDevice(st, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) return 256;
+  if (dev < 0 || dev >= kMaxDev) return 256;
+  int n = cache[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  cache[dev].store(n, std::memory_order_relaxed);
+  return n;
 }
 
 // XCD-aware block remap (bijective for any grid size): blocks b and b+8 land

@@ -223,8 +223,5 @@ int launch_conv(const ConvArgs& a, int epilogue, int math, hipStream_t stream);
 // fp16x3 stem 7x7/s2 + BN + ReLU + max-pool 3x3/s2 in one kernel over 16 x 16 patches + a merge
 // pass (stem_patch_kernel.h); SFA_E_UNSUPPORTED if the stem's shape does not tile 16 x 16.
 int launch_stem_patch(const ConvArgs& a, hipStream_t stream);
-// The KFPN levels' fused heads (EPI_HEAD, n = 3) as one launch; SFA_E_UNSUPPORTED when the
-// math mode or the A/B head kernel has no grouped form (launch each level then).
-int launch_conv_heads_group(const ConvArgs* levels, int n, int math, hipStream_t stream);
 
 }  // namespace sfa

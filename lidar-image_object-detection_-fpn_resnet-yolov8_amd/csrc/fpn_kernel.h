@@ -39,7 +39,7 @@ struct FpnGeom {
   static constexpr int KC = KT < KCM ? KT : KCM;   // K-tiles per A chunk
   static constexpr int NCH = KT / KC;              // chunks per row tile
   static constexpr int BROW = 64, TERM_B = BN * BROW, STAGE = 2 * TERM_B, W_BYTES = KT * STAGE;
-  static constexpr int LDS = W_BYTES + kFpnMaxFrames * 4 + 2 * NW * 4;
+  static constexpr int LDS = W_BYTES + kFpnMaxFrames * 4 + 2 * 2 * NW * 4;  // 2 amax reduction buffers
   static_assert(K % 32 == 0 && KT % KC == 0 && BN % 16 == 0 && BN >= 16, "fpn geometry");
 };
 
@@ -122,7 +122,10 @@ __global__ void __launch_bounds__(256, OCC) fpn_gemm_kernel(const ConvArgs a, in
   constexpr int KC = G::KC, NCH = G::NCH, BROW = G::BROW, TERM_B = G::TERM_B, STAGE = G::STAGE;
   __shared__ __attribute__((aligned(16))) unsigned char smem[G::LDS];
   float* const FS = reinterpret_cast<float*>(smem + G::W_BYTES);  // per-frame fp16x3 scales
-  unsigned char* const RED = smem + G::W_BYTES + kFpnMaxFrames * 4;  // epilogue amax reduction
+  // epilogue amax reduction, two buffers alternating by row tile: thread 0 reads tile t's words after
+  // the commit's barrier, and a wave that runs ahead into tile t + 1 writes the other buffer (tile
+  // t + 2 comes after tile t + 1's barrier, which thread 0 only reaches once it has read them)
+  unsigned char* const RED = smem + G::W_BYTES + kFpnMaxFrames * 4;
   auto swzB = [](int R) { return ((R >> 2) & 3) ^ ((((R & 15) + 4) >> 3) & 1); };
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -207,7 +210,7 @@ __global__ void __launch_bounds__(256, OCC) fpn_gemm_kernel(const ConvArgs a, in
         }
       }
     }
-    if (c == NCH - 1) fpn_epilogue<TM, TN, NT, RU>(a, acc, RED, m0 + wave * WM, m0, n0, lane, ainv);
+    if (c == NCH - 1) fpn_epilogue<TM, TN, NT, RU>(a, acc, RED + (t & 1) * 2 * NW * 4, m0 + wave * WM, m0, n0, lane, ainv);
   };
   // two chunks in flight: the next one's loads issued before this one's MFMAs; one copy of the
   // body (rb is moved into ra, which the next iteration's MFMAs would wait for anyway)
@@ -239,17 +242,36 @@ inline int launch_fpn_gemm_cfg(const ConvArgs& a, hipStream_t st) {
     return SFA_E_UNSUPPORTED;
   }
   const int P = a.OH * a.OW;
-  if ((a.M + P - 1) / P > kFpnMaxFrames || 2ull * a.N * (a.wstride ? a.wstride : a.Kpad) * 2ull >= (1ull << 31)) {
-    set_error("fpn_gemm: more than %d frames or weights >= 2 GiB", kFpnMaxFrames);
+  if (2ull * a.N * (a.wstride ? a.wstride : a.Kpad) * 2ull >= (1ull << 31)) {
+    set_error("fpn_gemm: weights >= 2 GiB");
     return SFA_E_UNSUPPORTED;
   }
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-      ncu = 256;
+  const int frames = (a.M + P - 1) / P;
+  if (frames > kFpnMaxFrames) {
+    // the per-frame scale table holds kFpnMaxFrames frames: launch frame chunks of that size. A row's
+    // products, K order and epilogue do not depend on the block that computes it, so every frame gets
+    // the bits it gets in a smaller batch (batch invariance).
+    if (a.M != frames * P) {
+      set_error("fpn_gemm: M=%d is not a whole number of %d-pixel frames", a.M, P);
+      return SFA_E_INVALID;
+    }
+    const size_t half = (size_t)(a.OH / 2) * (a.OW / 2) * a.N;  // res_up floats per frame
+    for (int f0 = 0; f0 < frames; f0 += kFpnMaxFrames) {
+      const int nf = frames - f0 < kFpnMaxFrames ? frames - f0 : kFpnMaxFrames;
+      ConvArgs c = a;
+      c.M = nf * P;
+      c.seg[0].x = a.seg[0].x + (size_t)f0 * P * K;
+      c.seg[0].bytes = (unsigned)((size_t)c.M * K * 4);
+      c.y = a.y + (size_t)f0 * P * a.N;
+      if (a.amax_in[0]) c.amax_in[0] = a.amax_in[0] + (size_t)f0 * SFA_AMAX_WORDS;
+      if (a.amax_out) c.amax_out = a.amax_out + (size_t)f0 * SFA_AMAX_WORDS;
+      if (RU) c.res_up = a.res_up + (size_t)f0 * half;
+      const int rc = launch_fpn_gemm_cfg<K, BN, RU, OCC>(c, st);
+      if (rc != SFA_OK) return rc;
+    }
+    return SFA_OK;
   }
+  const int ncu = cu_count(st);
   const int n_mt = ceil_div(a.M, G::BM), n_nt = a.N / BN;
   int gx = (ncu * OCC + n_nt - 1) / n_nt;  // blocks per column tile
   if (gx > n_mt) gx = n_mt;
@@ -473,13 +495,7 @@ inline int launch_fpn_row_cfg(const ConvArgs& a, hipStream_t st) {
   const int frames = a.M / (a.OH * a.OW);
   if (frames <= 0) return SFA_OK;
   if ((size_t)frames * (a.OH / 2) * (a.OW / 2) * a.N * 4 >= (1ull << 31)) return SFA_E_UNSUPPORTED;
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-      ncu = 256;
-  }
+  const int ncu = cu_count(st);
   const int nct = a.N / NB;
   int segs = (OCC * ncu + frames * nct - 1) / (frames * nct);  // about OCC blocks per CU
   segs = segs < 1 ? 1 : (segs > a.OH ? a.OH : segs);

@@ -706,13 +706,7 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
   }
   const int frames = a.M / (a.OH * a.OW);
   const int ntiles = frames * (a.OH / 16) * (a.OW / 16);
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
-      ncu = 256;
-  }
+  const int ncu = cu_count(st);
   const int grid = ntiles < ncu ? ntiles : ncu;
   if (grid <= 0) return SFA_OK;
   const dim3 gd((unsigned)grid), bd(stem_patch::NT);

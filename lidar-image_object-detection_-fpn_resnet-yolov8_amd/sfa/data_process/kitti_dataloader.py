@@ -10,6 +10,13 @@ sweeps are voxelised on the GPU in the main process — one ``sfa_bev_voxelize``
 the default collate (``test.py:124`` then moves it to the device and casts it, ``:127`` reads it as
 numpy for drawing).  Workers never touch HIP, so the callers' order — model on the GPU first
 (``test.py:112``), then the loader (``:120``) with ``--num_workers 1`` — works.
+
+Opt-in ``configs.bev_on_device = True`` (default False: the reference's f64 CPU tensor): the maps
+are yielded as a (B, 3, 608, 608) float32 tensor already on the GPU — the voxeliser writes the
+model's input layout directly, so the 8.9 MB-per-frame f64 device-to-host copy and the caller's
+host-to-device copy back (``test.py:124`` ``.to(device).float()``, then a no-op) disappear.  The
+values are the f64 maps rounded to float32, i.e. what ``.float()`` makes of the default tensor, so
+detections are bit-equal in both modes.  For callers that do not read the maps as numpy.
 """
 
 from __future__ import annotations
@@ -36,20 +43,32 @@ class DeferredBEVBatch:
     def __reduce__(self):
         return DeferredBEVBatch, (self.items,)
 
-    def voxelize(self, device=None, boundary=None) -> torch.Tensor:
+    def voxelize(self, device=None, boundary=None, on_device: bool = False) -> torch.Tensor:
         """(B, 3, 608, 608) float64 CPU tensor: every sweep's map (get_filtered_lidar + makeBEVMap),
-        made on the GPU ``device`` (default: the current one) in launches of up to 64 sweeps."""
+        made on the GPU ``device`` (default: the current one) in launches of up to 64 sweeps.
+        ``on_device``: the same maps as a float32 tensor left on that GPU (module docstring)."""
         dev = runtime.host_api_device("the loader's BEV maps", device)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
         boundary = boundary or cnf.boundary
-        out = torch.empty((len(self.items), 3, cnf.BEV_HEIGHT, cnf.BEV_WIDTH), dtype=torch.float64)
+        shape = (len(self.items), 3, cnf.BEV_HEIGHT, cnf.BEV_WIDTH)
+        if on_device:
+            out = torch.empty(shape, dtype=torch.float32, device=dev)
+            layout = _lib.BEV_NCHW3_F32
+        else:
+            out = torch.empty(shape, dtype=torch.float64)
+            layout = _lib.BEV_NCHW3_F64
         vox = runtime.voxelizer(dev)
         for c0 in range(0, len(self.items), _lib.SFA_BEV_MAX_BATCH):
             chunk = self.items[c0:c0 + _lib.SFA_BEV_MAX_BATCH]
             offs = np.cumsum([0] + [d.points.shape[0] for d in chunk])
             pts = np.concatenate([d.points for d in chunk]) if offs[-1] else np.zeros((1, 4), np.float32)
-            maps = vox(torch.from_numpy(pts).to(dev), offs, boundary, layout=_lib.BEV_NCHW3_F64,
-                       flags=_lib.BEV_RAW)
-            out[c0:c0 + len(chunk)].copy_(maps)
+            if on_device:  # written in place: no intermediate map
+                vox(torch.from_numpy(pts).to(dev), offs, boundary, layout=layout, flags=_lib.BEV_RAW,
+                    out=out[c0:c0 + len(chunk)])
+            else:
+                maps = vox(torch.from_numpy(pts).to(dev), offs, boundary, layout=layout, flags=_lib.BEV_RAW)
+                out[c0:c0 + len(chunk)].copy_(maps)
         for i, d in enumerate(self.items):
             if d.flip_w:  # train-mode hflip: torch.flip(bev_map, [-1]) (kitti_dataset.py:97)
                 out[i] = torch.flip(out[i], [-1])
@@ -74,16 +93,19 @@ class DeviceBEVLoader:
     (DeferredBEVBatch.voxelize) in the calling (main) process.  Everything else — len(), .dataset,
     .batch_size, .sampler, ... — is the DataLoader's."""
 
-    def __init__(self, loader: DataLoader, device=None):
+    def __init__(self, loader: DataLoader, device=None, on_device: bool = False):
         self.loader = loader
         self.device = device
+        self.on_device = bool(on_device)
 
     def __iter__(self):
+        dev, od = self.device, self.on_device
         for batch in self.loader:
             if isinstance(batch, (tuple, list)):
-                yield type(batch)(b.voxelize(self.device) if isinstance(b, DeferredBEVBatch) else b for b in batch)
+                yield type(batch)(b.voxelize(dev, on_device=od) if isinstance(b, DeferredBEVBatch) else b
+                                  for b in batch)
             elif isinstance(batch, DeferredBEVBatch):
-                yield batch.voxelize(self.device)
+                yield batch.voxelize(dev, on_device=od)
             else:
                 yield batch
 
@@ -91,16 +113,29 @@ class DeviceBEVLoader:
         return len(self.loader)
 
     def __getattr__(self, name):
-        if name in ("loader", "device"):
+        if name in ("loader", "device", "on_device"):
             raise AttributeError(name)
         return getattr(self.loader, name)
 
 
+def _cfg(configs, name, default):
+    """configs.<name>, or default when unset (EasyDict raises AttributeError, dict-backed configs
+    KeyError)."""
+    try:
+        return getattr(configs, name)
+    except (AttributeError, KeyError):
+        return default
+
+
 def _loader(dataset, configs, shuffle, sampler):
     dataset.defer_bev = True
+    on_device = bool(_cfg(configs, "bev_on_device", False))  # opt-in (module docstring)
+    device = _cfg(configs, "device", None) if on_device else None
+    if device is not None and torch.device(device).type != "cuda":
+        device = None
     return DeviceBEVLoader(DataLoader(dataset, batch_size=configs.batch_size, shuffle=shuffle,
                                       pin_memory=configs.pin_memory, num_workers=configs.num_workers,
-                                      sampler=sampler, collate_fn=bev_collate))
+                                      sampler=sampler, collate_fn=bev_collate), device=device, on_device=on_device)
 
 
 def create_train_dataloader(configs):

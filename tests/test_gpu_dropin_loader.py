@@ -56,3 +56,55 @@ def test_test_loader_loop_like_test_py(tmp_path, gpu, golden, monkeypatch):
         ref = pipe.run().cpu().numpy()[:len(sids)]
         np.testing.assert_array_equal(dets, ref)
     assert seen == ids
+
+
+def test_test_loader_bev_on_device(tmp_path, gpu, golden, monkeypatch):
+    """Opt-in configs.bev_on_device: the loader yields the (B, 3, 608, 608) maps
+    as float32 tensors already on the GPU (no f64 device-to-host copy and back). They equal the
+    default mode's f64 CPU maps cast to float32 (what test.py:124 makes of them), and the callers'
+    .to(device).float() -> model -> _sigmoid -> decode sequence gives bit-equal detections in both
+    modes; the default stays the reference's f64 CPU tensor."""
+    from data_process.kitti_dataloader import create_test_dataloader
+    from data_process.kitti_dataset import KittiDataset
+    from models.model_utils import create_model
+    from utils.evaluation_utils import decode
+    from utils.torch_utils import _sigmoid
+    monkeypatch.setattr(KittiDataset, "get_image", lc.stub_image)
+    ids, clouds = lc.make_tree(str(tmp_path))
+    cfg = lc.Cfg(arch="fpn_resnet_18", heads=dict(gc.HEADS), head_conv=64, imagenet_pretrained=False)
+    model = create_model(cfg)
+    sd = gc.state_dict_np(golden.model)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    model = model.to(gpu).eval()
+    torch.cuda.synchronize()
+
+    def run(on_device):
+        conf = lc.configs(str(tmp_path), batch_size=2, num_workers=1)
+        if on_device is not None:
+            conf.bev_on_device = on_device
+            conf.device = gpu
+        maps, dets = [], []
+        for _, bev_maps, _ in create_test_dataloader(conf):
+            if on_device:
+                assert bev_maps.dtype == torch.float32 and bev_maps.device == gpu
+            else:
+                assert bev_maps.dtype == torch.float64 and bev_maps.device.type == "cpu"
+            maps.append(bev_maps.cpu())
+            with torch.no_grad():
+                out = model(bev_maps.to(gpu).float())
+                out["hm_cen"] = _sigmoid(out["hm_cen"])
+                out["cen_offset"] = _sigmoid(out["cen_offset"])
+                dets.append(decode(out["hm_cen"], out["cen_offset"], out["direction"], out["z_coor"], out["dim"],
+                                   K=50).cpu().numpy())
+        return maps, dets
+
+    m_host, d_host = run(None)
+    m_off, d_off = run(False)
+    m_dev, d_dev = run(True)
+    assert len(m_host) == len(m_dev) == len(m_off) == (len(ids) + 1) // 2
+    for a, b, c in zip(m_host, m_off, m_dev):
+        np.testing.assert_array_equal(a.numpy(), b.numpy())
+        np.testing.assert_array_equal(a.float().numpy(), c.numpy())
+    for a, b, c in zip(d_host, d_off, d_dev):
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(a, c)

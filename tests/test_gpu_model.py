@@ -317,6 +317,41 @@ def test_fpn_gemm_kernel_choices(golden, gpu, hw):
                 assert float(np.max(np.abs(res[mask][h] - r) / np.maximum(1.0, np.abs(r)))) <= 1e-4, (h, mask)
 
 
+def test_fpn_gemm_residual_wide_rows(golden, gpu):
+    """At 64 x 704 the level-2 skip conv's output rows (176 px) are wider than fpn_row_kernel takes
+    (160), so with the skip-conv bits set it runs on the persistent fpn_gemm<..., true, ...> kernel,
+    which commits its per-frame output maxima once per row tile into alternating LDS buffers
+    (ADVICE r04): bit-identical to the per-tile conv_r3 skip convs (mask 0), the next convs' fp16x3
+    scales included."""
+    x = torch.from_numpy(synthetic.synthetic_bev(2, 64, 704, seed=23)).to(gpu)
+    res = {}
+    for mask in (0, 56):
+        model = make_model(golden, gpu)
+        eng = model._engine(gpu)
+        eng.set_math(_math("fp16x3"))
+        eng.set_option(_lib.OPT_FPN_GEMM, mask)
+        with torch.no_grad():
+            res[mask] = {h: v.cpu().numpy() for h, v in model(x).items()}
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(res[56][h], res[0][h], err_msg=f"{h}: wide-row fpn_gemm skip convs vs conv_r3")
+
+
+def test_fpn_gemm_batch_over_256_frames(golden, gpu):
+    """fpn_gemm keeps the frame scales of at most 256 frames in LDS; larger batches run as 256-frame
+    chunks of the same kernel, so frames 255, 256 of a 258-frame batch equal the same frames as a
+    batch of 2, bit for bit, with the default FPN kernel choice."""
+    x = torch.from_numpy(synthetic.synthetic_bev(258, 64, 64, seed=29)).to(gpu)
+    model = make_model(golden, gpu)
+    eng = model._engine(gpu)
+    eng.set_math(_math("fp16x3"))
+    assert eng.get_option(_lib.OPT_FPN_GEMM) == 37
+    with torch.no_grad():
+        full = {h: v[255:257].cpu().numpy() for h, v in model(x).items()}
+        two = {h: v.cpu().numpy() for h, v in model(x[255:257].contiguous()).items()}
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(full[h], two[h], err_msg=f"{h}: batch of 258 vs batch of 2")
+
+
 def test_batch_invariance_608(golden, gpu):
     """At the full 608x608 size (every kernel path of the bench: r3 heads, strip convs, FPN skip
     convs, r3 body convs (M >= 50000 needs >= 9 frames), split-K layer4): frames 7, 8 of a batch

@@ -24,7 +24,7 @@
 #include "../lidar-image_object-detection_-fpn_resnet-yolov8_amd/csrc/conv_h3_kernel.h"
 #include "experiments/r03/conv_h3s_kernel.h"  // the round-3 variants (tune / ABL bits) live here
 #include "experiments/r03/conv_r3_kernel.h"
-#include "experiments/conv_ws_kernel.h"
+#include "experiments/r03/conv_ws_kernel.h"
 
 namespace sfa {
 void set_error(const char* fmt, ...) {

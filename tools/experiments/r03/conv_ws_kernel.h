@@ -16,7 +16,7 @@
 // weights for every 128-row block: 144 KiB per block, more than its A strip.
 #pragma once
 
-#include "r03/conv_r3_kernel.h"
+#include "conv_r3_kernel.h"
 
 namespace sfa {
 
