@@ -176,8 +176,13 @@ int sfa_model_get_math(const sfa_model* model);
  *                                         conv, bit 3 + f = its skip conv (37: the low-res convs of
  *                                         levels 0 and 2, the level-2 skip conv on full rows); the
  *                                         others on the per-tile kernels
+ *   SFA_OPT_SPLITK_TICKETS (SFA_SPLITK_TICKETS) 1 (default): the split-K layer4 strip convs combine
+ *                                         their slices in the conv kernel (the last slice of a tile to
+ *                                         finish, by an atomic ticket); 0: a reduce launch per conv; the
+ *                                         same bits
  */
-enum sfa_model_option { SFA_OPT_STEM_PATCH = 0, SFA_OPT_FPN_COMMUTE = 1, SFA_OPT_FPN_GEMM = 2 };
+enum sfa_model_option { SFA_OPT_STEM_PATCH = 0, SFA_OPT_FPN_COMMUTE = 1, SFA_OPT_FPN_GEMM = 2,
+                        SFA_OPT_SPLITK_TICKETS = 3 };
 int sfa_model_set_option(sfa_model* model, int key, int value);
 int sfa_model_get_option(const sfa_model* model, int key, int* value);
 

@@ -187,10 +187,12 @@ struct ConvArgs {
   const float* res_up;
   float res_sh, res_sw;
   // Round-3 experiment knobs (tools/experiments/r03 kernels and their convbench hooks only): tune
-  // bits, stem ablations, in-kernel split-K tickets. The product kernels never read them and the
-  // model leaves them zero.
+  // bits, stem ablations. The product kernels never read them and the model leaves them zero.
   int tune;
   int stem_abl;
+  // split-K tickets (>= one word per output tile, zeroed before the launch): with them the last slice
+  // of a tile combines the partials in the conv kernel (conv_h3_kernel.h splitk_ticket) instead of
+  // splitk_reduce_kernel; null: the reduce launch
   unsigned* tile_cnt;
   // Patch stem input (stem_patch_kernel.h): STEM_IN_NHWC4 (the voxeliser's layout), STEM_IN_NCHW3
   // (the reference's (B, 3, H, W)), STEM_IN_NCHW3_FLIP (read as torch.flip(x, [2, 3])); every

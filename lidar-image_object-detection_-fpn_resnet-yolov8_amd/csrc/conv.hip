@@ -156,6 +156,7 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     else if (!strip && tile_rows(a) >= 50000)  // big-M stride-2 / two-segment: A from registers
       rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
     if (!ok(rc)) {
+      b.tile_cnt = nullptr;  // conv_h3: the reduce launch (conv_h3_kernel.h splitk_ticket)
       if ((a.Kpad / 32) % b.ksplit != 0) b.ksplit = 1;  // K not divisible into the slices: no split
       rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2, 1>(b, st);
     }

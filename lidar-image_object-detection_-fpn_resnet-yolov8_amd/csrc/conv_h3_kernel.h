@@ -242,6 +242,26 @@ __device__ __forceinline__ void h3_pool_epilogue(const ConvArgs& a, x6_f32x16 (&
 // (fewer LDS bytes per MAC) and splits its WM rows of A.
 // RU: the epilogue handles an upsampled residual (a.res_up); instances without it (every conv but the
 // FPN skip convs) keep the residual tile in registers without spilling.
+// In-kernel split-K combine (round 5; conv_h3s_kernel, whose partials are float4 rows, replaces
+// splitk_reduce_kernel with it when the conv has a ticket array, ConvArgs::tile_cnt — conv_h3_kernel's
+// element-strided partials made write-through cost 30-38 us per layer4 conv, profiles/r05c_*, so it
+// keeps the reduce launch): every slice stores its partial tile write-through (sc1), waits for the stores
+// (s_waitcnt vmcnt(0)) in every wave, and after a workgroup barrier one lane takes a ticket for the
+// output tile with an agent-scope atomic add; the slice whose add returns nsplit - 1 is the last to
+// finish and, after a second barrier, reads the other slices' partials with sc1 loads and applies the
+// reduce kernel's epilogue (slices added in slice order 0 .. nsplit-1 with its own partial from
+// registers, + bias, + residual, ReLU, per-frame max): bit-identical to the reduce launch.  This is
+// the producer / consumer hand-off of MI355X_MICROARCH.md (inter-workgroup visibility: sc1 stores,
+// drained, one atomic add per storing workgroup, the last adder reads with sc1 loads); the tickets are
+// zeroed with the forward's amax words.  `flag` is an LDS word no wave uses meanwhile.
+__device__ __forceinline__ bool splitk_ticket(unsigned* cnt, int tile, int nsplit, unsigned* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores have completed
+  __syncthreads();                                   // ... and every other wave's
+  if (threadIdx.x == 0) *flag = __hip_atomic_fetch_add(cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return *flag == (unsigned)(nsplit - 1);
+}
+
 template <int BM, int BN, int WM, int EPI, int OCC, int BK, int NSTAGE, int NSEG, bool NMAJ = false,
           int ABL = 0, int MF = 0, int WN = BN, bool RU = false>
 __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_h3_kernel(const ConvArgs a) {
@@ -704,7 +724,7 @@ inline int launch_conv_h3_cfg(const ConvArgs& a, hipStream_t st) {
                        dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WN) * 64), 0, st, a);
   }
   SFA_LAUNCH_CHECK();
-  if (ks > 1) {
+  if (ks > 1) {  // the slices' partials combined by the reduce launch (element-strided partials: no tickets)
     const long long nel = (long long)a.M * a.N;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((nel + 1023) / 1024)), dim3(256), 0, st, a);
     SFA_LAUNCH_CHECK();

@@ -341,19 +341,55 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (nsplit > 1) {  // split-K partials, transposed form: float4 per lane (the reduce launch adds them)
-    float* part = a.part + (size_t)kz * M * a.N;
+  if (nsplit > 1) {  // split-K partials, transposed form: float4 per lane
+    // combined by the reduce launch, or (ConvArgs::tile_cnt) by the last slice to finish
+    // (splitk_ticket, conv_h3_kernel.h: sc1 partial stores, one ticket per tile)
+    const __amdgpu_buffer_rsrc_t rsp = __builtin_amdgcn_make_buffer_rsrc(
+        a.part, (short)0, (int)((size_t)nsplit * M * a.N * 4 < 0x7fffffffu ? (size_t)nsplit * M * a.N * 4 : 0x7fffffffu),
+        0x00020000);
+    const bool tk = a.tile_cnt != nullptr;
+    x6_f32x4 val[TM][TN];
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
         const int m = m0 + wave * WM + mi * 16 + c16, n = n0 + ni * 16 + 4 * gq;
         const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(a.winv + n);
-        x6_f32x4 val;
 #pragma unroll
-        for (int v = 0; v < 4; ++v) val[v] = acc[mi][ni][v] * ainv[mi] * cs[v];
-        if (m < M) *reinterpret_cast<x6_f32x4*>(part + (size_t)m * a.N + n) = val;
+        for (int v = 0; v < 4; ++v) val[mi][ni][v] = acc[mi][ni][v] * ainv[mi] * cs[v];
+        if (m < M) {
+          const unsigned off = (unsigned)((((size_t)kz * M + m) * a.N + n) * 4);
+          if (tk) __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(x6_u32x4, val[mi][ni]), rsp, off, 0, 16);
+          else __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(x6_u32x4, val[mi][ni]), rsp, off, 0, 0);
+        }
       }
+    if (!tk || !splitk_ticket(a.tile_cnt, mt * n_tiles + nt, nsplit, reinterpret_cast<unsigned*>(smem + 1024)))
+      return;
+    // the last slice: splitk_reduce_kernel's epilogue on this tile (slice order, + bias, + residual, ReLU)
+    AmaxRows am(a.OH * a.OW, m0);
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int m = m0 + wave * WM + mi * 16 + c16, n = n0 + ni * 16 + 4 * gq;
+        if (m >= M) continue;
+        auto part_z = [&](int z) {
+          return z == kz ? val[mi][ni]
+                         : __builtin_bit_cast(x6_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                            rsp, (unsigned)((((size_t)z * M + m) * a.N + n) * 4), 0, 16));
+        };
+        x6_f32x4 sv = part_z(0);
+        for (int z = 1; z < nsplit; ++z) sv += part_z(z);
+        sv += *reinterpret_cast<const x6_f32x4*>(a.bias + n);
+        if (a.res) sv += *reinterpret_cast<const x6_f32x4*>(a.res + (size_t)m * a.N + n);
+        if (a.relu) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) sv[v] = fmaxf(sv[v], 0.f);
+        }
+        *reinterpret_cast<x6_f32x4*>(a.y + (size_t)m * a.N + n) = sv;
+        if (a.amax_out) am.add(a.amax_out, m, fmaxf(fmaxf(fabsf(sv[0]), fabsf(sv[1])), fmaxf(fabsf(sv[2]), fabsf(sv[3]))));
+      }
+    if (a.amax_out) amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1, reinterpret_cast<float*>(smem));
     return;
   }
   __syncthreads();
@@ -387,7 +423,7 @@ inline int launch_conv_h3s_cfg(const ConvArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((conv_h3s_kernel<BM, BN, WM, EPI, OCC, ABL>), dim3((unsigned)nblocks), dim3((BM / WM) * 64), 0,
                      st, a);
   SFA_LAUNCH_CHECK();
-  if (ks > 1) {  // the slices' partials combined by the reduce launch
+  if (ks > 1 && !a.tile_cnt) {  // the slices' partials combined by the reduce launch
     const long long nel = (long long)a.M * a.N;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((nel + 1023) / 1024)), dim3(256), 0, st, a);
     SFA_LAUNCH_CHECK();

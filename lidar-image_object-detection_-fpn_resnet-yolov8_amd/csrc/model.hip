@@ -293,6 +293,10 @@ struct sfa_model {
   // run on conv_h3 / conv_r3 (the same products for the skip convs). Default 37 = the low-res convs of
   // levels 0 and 2 and the level-2 skip conv, the ones measured faster (profiles/r04d_*, r04l_*)
   int fpn_gemm = 37;
+  // fp16x3 split-K layer4 strip convs: 1 (default) = the last slice of each tile combines the partials in
+  // the conv kernel (tickets, conv_h3_kernel.h splitk_ticket), 0 = splitk_reduce_kernel launches; the
+  // same bits (env SFA_SPLITK_TICKETS). conv_h3's split convs keep the reduce launch.
+  int splitk_tickets = 1;
   // Side stream for the level-0 heads (they only need up_level2, so they overlap the rest
   // of the FPN and the level-1/2 heads); created with the model on the current device,
   // used only when the forward's stream is on that device.
@@ -474,6 +478,7 @@ extern "C" int sfa_model_create(const sfa_arch* arch, const float* packed_device
   if (const char* e = getenv("SFA_STEM_PATCH")) m->stem_patch = atoi(e) != 0;
   if (const char* e = getenv("SFA_FPN_COMMUTE")) m->fpn_commute = atoi(e) & 7;
   if (const char* e = getenv("SFA_FPN_GEMM")) m->fpn_gemm = atoi(e) & 63;
+  if (const char* e = getenv("SFA_SPLITK_TICKETS")) m->splitk_tickets = atoi(e) != 0;
   bool side_streams = true;  // env SFA_SIDE_STREAMS=0: every launch on the caller's stream (A/B)
   if (const char* e = getenv("SFA_SIDE_STREAMS")) side_streams = strcmp(e, "0") != 0;
   if (side_streams) make_side_streams(m);
@@ -520,6 +525,10 @@ extern "C" int sfa_model_set_option(sfa_model* model, int key, int value) {
       SFA_CHECK_ARG(value >= 0 && value <= 63, "set_option: FPN_GEMM mask %d not in 0..63", value);
       model->fpn_gemm = value;
       break;
+    case SFA_OPT_SPLITK_TICKETS:
+      SFA_CHECK_ARG(value == 0 || value == 1, "set_option: SPLITK_TICKETS %d not 0 / 1", value);
+      model->splitk_tickets = value;
+      break;
     default: set_error("set_option: unknown key %d", key); return SFA_E_INVALID;
   }
   return SFA_OK;
@@ -531,6 +540,7 @@ extern "C" int sfa_model_get_option(const sfa_model* model, int key, int* value)
     case SFA_OPT_STEM_PATCH: *value = model->stem_patch; break;
     case SFA_OPT_FPN_COMMUTE: *value = model->fpn_commute; break;
     case SFA_OPT_FPN_GEMM: *value = model->fpn_gemm; break;
+    case SFA_OPT_SPLITK_TICKETS: *value = model->splitk_tickets; break;
     default: set_error("get_option: unknown key %d", key); return SFA_E_INVALID;
   }
   return SFA_OK;
@@ -570,7 +580,8 @@ namespace sfa {
 
 // Activation buffers of one forward (NHWC f32), carved from the workspace.
 struct Bufs {
-  size_t xin, s0, p0, t[4], a[4], l[4], up1, c1, up2, c2, up3, up4, L0, L1, L2, amax, part, part_floats, total;
+  size_t xin, s0, p0, t[4], a[4], l[4], up1, c1, up2, c2, up3, up4, L0, L1, L2, amax, tick, tick_words, part,
+      part_floats, total;
 };
 
 // fp16x3 activation maxima (conv.h): per tensor a conv reads (named by its producer), B
@@ -610,8 +621,12 @@ static Bufs plan_bufs(const sfa_arch* arch, int B, int H, int W) {
   b.L0 = take((size_t)nch * B * P8);
   b.L1 = take((size_t)nch * B * P4);
   b.L2 = take((size_t)nch * B * P4);
-  // the activation maxima (zeroed once per forward)
+  // the activation maxima and the split-K tickets (one zeroing memset per forward, right after them)
   b.amax = take((size_t)AM_COUNT * B * SFA_AMAX_WORDS);
+  // split-K tickets (conv_h3_kernel.h splitk_ticket): one word per output tile of each of the four
+  // layer4 convs, for tiles of >= 64 x 64
+  b.tick_words = (size_t)((B * (H / 32) * (W / 32) + 63) / 64) * (512 / 64);
+  b.tick = take(4 * b.tick_words);
   // split-K partial sums (conv.hip pick_ksplit: 2 slices of the 512-wide layer4 convs)
   b.part_floats = (size_t)2 * B * (H / 32) * (W / 32) * 512;
   b.part = take(b.part_floats);
@@ -706,8 +721,8 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
     return h3 ? reinterpret_cast<unsigned*>(ws + bf.amax) + (size_t)slot * B * SFA_AMAX_WORDS : nullptr;
   };
   auto blk_slot = [](int li, int bi, int ci) { return AM_BLK + 4 * li + 2 * bi + ci; };
-  if (h3)
-    SFA_HIP_TRY(hipMemsetAsync(ws + bf.amax, 0, (size_t)AM_COUNT * B * SFA_AMAX_WORDS * 4, st));
+  if (h3)  // the amax words and the split-K tickets after them
+    SFA_HIP_TRY(hipMemsetAsync(ws + bf.amax, 0, bf.tick + 4 * bf.tick_words * 4 - bf.amax, st));
   auto io = [&](ConvArgs& a, int in0, int in1, int out) {
     a.amax_in[0] = in0 >= 0 ? AM(in0) : nullptr;
     a.amax_in[1] = in1 >= 0 ? AM(in1) : nullptr;
@@ -753,6 +768,11 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   const float* xcur = F(bf.p0);
   int xslot = AM_STEM;  // maxpool keeps the stem's max
   int h = H / 4, w = W / 4, cin = 64;
+  // split-K tickets of the layer4 convs (the only split ones, conv.hip pick_ksplit): the slice that
+  // finishes last combines the partials in the conv kernel (no reduce launch); fp16x3 only
+  auto TK = [&](int li, int ci) -> unsigned* {
+    return h3 && li == 3 && m->splitk_tickets ? reinterpret_cast<unsigned*>(ws + bf.tick) + (size_t)ci * bf.tick_words : nullptr;
+  };
   for (int li = 0; li < 4; ++li) {
     const int planes = 64 << li;
     const int stride = li == 0 ? 1 : 2;
@@ -765,6 +785,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       ConvArgs a = conv_args(wb, p.blk[li][0][0], B, oh, ow, t, nullptr, 1);
       a.seg[0] = seg(xcur, B, h, w, cin, 3, stride, 1);
       io(a, xslot, -1, blk_slot(li, 0, 0));
+      a.tile_cnt = TK(li, 0);
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     {
@@ -776,6 +797,7 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
         a.seg[1] = seg(xcur, B, h, w, cin, 1, stride, 0);
       }
       io(a, blk_slot(li, 0, 0), li > 0 ? xslot : -1, blk_slot(li, 0, 1));
+      a.tile_cnt = TK(li, 1);
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     // block 1
@@ -783,12 +805,14 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
       ConvArgs a = conv_args(wb, p.blk[li][1][0], B, oh, ow, t, nullptr, 1);
       a.seg[0] = seg(av, B, oh, ow, planes, 3, 1, 1);
       io(a, blk_slot(li, 0, 1), -1, blk_slot(li, 1, 0));
+      a.tile_cnt = TK(li, 2);
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     {
       ConvArgs a = conv_args(wb, p.blk[li][1][1], B, oh, ow, lv, av, 1);
       a.seg[0] = seg(t, B, oh, ow, planes, 3, 1, 1);
       io(a, blk_slot(li, 1, 0), -1, blk_slot(li, 1, 1));
+      a.tile_cnt = TK(li, 3);
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     xcur = lv;

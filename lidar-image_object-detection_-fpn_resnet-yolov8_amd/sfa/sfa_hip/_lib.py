@@ -26,8 +26,8 @@ SFA_BEV_MAX_BATCH = 64
 BEV_NCHW3_F32, BEV_NCHW3_F64, BEV_NHWC4_F32 = 0, 1, 2
 BEV_RAW, BEV_PREFILTERED, BEV_FLIP_HW, BEV_FORCE_ATOMIC, BEV_FORCE_BINNED, BEV_STRIP8 = 0, 1, 2, 4, 8, 16
 # sfa_model_set_option keys (include/sfa_hip.h sfa_model_option)
-OPT_STEM_PATCH, OPT_FPN_COMMUTE, OPT_FPN_GEMM = 0, 1, 2
-OPT_COUNT = 3  # keys 0 .. OPT_COUNT - 1
+OPT_STEM_PATCH, OPT_FPN_COMMUTE, OPT_FPN_GEMM, OPT_SPLITK_TICKETS = 0, 1, 2, 3
+OPT_COUNT = 4  # keys 0 .. OPT_COUNT - 1
 IN_NCHW3, IN_NHWC4, IN_NCHW3_FLIP_HW = 0, 1, 2
 
 

@@ -194,7 +194,8 @@ def test_argument_errors_before_any_launch():
         assert L.sfa_model_probe_times(h, ms, 4) == -1
         # kernel-choice options live in the handle (no env reads on the launch path)
         v = ctypes.c_int()
-        defaults = {_lib.OPT_STEM_PATCH: 1, _lib.OPT_FPN_COMMUTE: 7, _lib.OPT_FPN_GEMM: 37}
+        defaults = {_lib.OPT_STEM_PATCH: 1, _lib.OPT_FPN_COMMUTE: 7, _lib.OPT_FPN_GEMM: 37,
+                    _lib.OPT_SPLITK_TICKETS: 1}
         assert len(defaults) == _lib.OPT_COUNT
         for key, val in defaults.items():
             assert L.sfa_model_get_option(h, key, ctypes.byref(v)) == 0 and v.value == val, key
@@ -206,6 +207,8 @@ def test_argument_errors_before_any_launch():
         assert L.sfa_model_set_option(h, _lib.OPT_FPN_COMMUTE, 5) == 0
         assert L.sfa_model_set_option(h, _lib.OPT_FPN_GEMM, 64) == -1
         assert L.sfa_model_set_option(h, _lib.OPT_FPN_GEMM, 63) == 0
+        assert L.sfa_model_set_option(h, _lib.OPT_SPLITK_TICKETS, 2) == -1
+        assert L.sfa_model_set_option(h, _lib.OPT_SPLITK_TICKETS, 0) == 0
         # the round-3 A/B keys (tune bits, grouped heads, ...) are gone: unknown keys now
         for gone in range(_lib.OPT_COUNT, 8):
             assert L.sfa_model_set_option(h, gone, 0) == -1

@@ -317,6 +317,28 @@ def test_fpn_gemm_kernel_choices(golden, gpu, hw):
                 assert float(np.max(np.abs(res[mask][h] - r) / np.maximum(1.0, np.abs(r)))) <= 1e-4, (h, mask)
 
 
+def test_splitk_tickets_bit_identical(golden, gpu):
+    """SFA_OPT_SPLITK_TICKETS: the split-K layer4 strip convs combine their two K-slices in the conv
+    kernel (the last slice of each tile to finish, by an agent-scope atomic ticket, reads the other's
+    sc1-stored partial) instead of a splitk_reduce_kernel launch: the same order of additions, so
+    bit-identical heads at 608 x 608 (bs 3: ragged last tiles), and a repeated forward (tickets re-zeroed
+    per forward) too."""
+    xs = [torch.from_numpy(synthetic.synthetic_bev(3, 608, 608, seed=s)).to(gpu) for s in (41, 43, 41)]
+    res = {}
+    for tk in (0, 1):
+        model = make_model(golden, gpu)
+        eng = model._engine(gpu)
+        eng.set_math(_math("fp16x3"))
+        eng.set_option(_lib.OPT_SPLITK_TICKETS, tk)
+        assert eng.get_option(_lib.OPT_SPLITK_TICKETS) == tk
+        with torch.no_grad():  # different inputs back to back: no partial of a previous forward is read
+            res[tk] = [{h: v.cpu().numpy() for h, v in model(x).items()} for x in xs]
+    for h in gc.HEADS:
+        for i in range(3):
+            np.testing.assert_array_equal(res[1][i][h], res[0][i][h], err_msg=f"{h}: tickets vs reduce, forward {i}")
+        np.testing.assert_array_equal(res[1][2][h], res[1][0][h], err_msg=f"{h}: repeated input with tickets")
+
+
 def test_fpn_gemm_residual_wide_rows(golden, gpu):
     """At 64 x 704 the level-2 skip conv's output rows (176 px) are wider than fpn_row_kernel takes
     (160), so with the skip-conv bits set it runs on the persistent fpn_gemm<..., true, ...> kernel,

@@ -126,6 +126,7 @@ struct Cand {
   Launch fn;
 };
 static float* g_part = nullptr;
+static unsigned* g_tick = nullptr;  // split-K tickets (zeroed before every launch, as the forward's memset does)
 static const size_t g_part_floats = 64u << 20;
 #define CS(BM, BN, WM, OCC, ABL, KS)                                                                  \
   Cand {                                                                                            \
@@ -135,6 +136,28 @@ static const size_t g_part_floats = 64u << 20;
       b.part = g_part;                                                                              \
       b.part_floats = g_part_floats;                                                                \
       return launch_conv_h3s_cfg<BM, BN, WM, EPI_STD, OCC, ABL>(b, s);                              \
+    }                                                                                               \
+  }
+#define CT(BM, BN, WM, OCC, ABL, KS)                                                                  \
+  Cand {                                                                                            \
+    "h3s " #BM "x" #BN " occ" #OCC " abl" #ABL " ks" #KS " tickets+memset", [](const ConvArgs& a, hipStream_t s) { \
+      ConvArgs b = a;                                                                               \
+      b.ksplit = KS;                                                                                \
+      b.part = g_part;                                                                              \
+      b.part_floats = g_part_floats;                                                                \
+      b.tile_cnt = g_tick;                                                                          \
+      if (hipMemsetAsync(g_tick, 0, 64 * 1024, s) != hipSuccess) return -1;                           \
+      return launch_conv_h3s_cfg<BM, BN, WM, EPI_STD, OCC, ABL>(b, s);                              \
+    }                                                                                               \
+  }
+#define CR(BM, BN, WM, OCC, NS, ABL, KS)                                                              \
+  Cand {                                                                                            \
+    "r3 " #BM "x" #BN " occ" #OCC " st" #NS " abl" #ABL " ks" #KS, [](const ConvArgs& a, hipStream_t s) { \
+      ConvArgs b = a;                                                                               \
+      b.ksplit = KS;                                                                                \
+      b.part = g_part;                                                                              \
+      b.part_floats = g_part_floats;                                                                \
+      return launch_conv_r3_cfg<BM, BN, WM, EPI_STD, OCC, NS, ABL>(b, s);                           \
     }                                                                                               \
   }
 #define CP(BM, BN, WM, OCC, RESPF, KS)                                                                \
@@ -161,13 +184,18 @@ int main(int argc, char** argv) {
                           CP(128, 64, 32, 3, false, 1)};
   std::vector<Cand> l2 = {CS(128, 128, 32, 2, 10, 1), CP(128, 128, 32, 2, false, 1), CS(128, 128, 32, 2, 10, 1),
                           CP(128, 128, 32, 2, false, 1)};
-  std::vector<Cand> l3 = {CS(64, 128, 16, 3, 10, 1), CP(64, 128, 16, 3, false, 1), CS(64, 128, 16, 3, 10, 1),
-                          CP(64, 128, 16, 3, false, 1)};
-  std::vector<Cand> l4 = {CS(128, 64, 32, 3, 142, 2), CP(128, 64, 32, 3, false, 2), CS(128, 64, 32, 3, 142, 2),
-                          CP(128, 64, 32, 3, false, 2)};
+  // round 5: the heads' register-A kernel (half-tile stagger, 3-stage W ring) on 256-wide tiles, the
+  // grid filled by split-K (reduce launch)
+  std::vector<Cand> l3 = {CS(64, 128, 16, 3, 10, 1), CR(192, 256, 32, 1, 3, 1603844, 2), CR(256, 256, 32, 1, 3, 1603844, 2),
+                          CR(256, 256, 32, 1, 3, 1603844, 3), CR(192, 256, 32, 1, 3, 1603844, 3),
+                          CS(64, 128, 16, 3, 10, 1), CR(192, 256, 32, 1, 3, 1603844, 2)};
+  std::vector<Cand> l4 = {CS(128, 64, 32, 3, 142, 2), CT(128, 64, 32, 3, 142, 2), CR(192, 256, 32, 1, 3, 1603844, 4),
+                          CR(256, 256, 32, 1, 3, 1603844, 6), CR(192, 256, 32, 1, 3, 1603844, 3),
+                          CS(128, 64, 32, 3, 142, 2), CT(128, 64, 32, 3, 142, 2), CR(192, 256, 32, 1, 3, 1603844, 4)};
   hipStream_t st;
   CK(hipStreamCreate(&st));
   CK(hipMalloc(&g_part, g_part_floats * 4));
+  CK(hipMalloc(&g_tick, 64 * 1024));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
