@@ -108,3 +108,26 @@ def test_test_loader_bev_on_device(tmp_path, gpu, golden, monkeypatch):
     for a, b, c in zip(d_host, d_off, d_dev):
         np.testing.assert_array_equal(a, b)
         np.testing.assert_array_equal(a, c)
+
+
+def test_deferred_bev_train_hflip(gpu):
+    """The train-mode deferred BEV (kitti_dataset.py:93-97: hflipped maps): a batch of
+    DeferredBEV sweeps with and without flip_w, voxelised by DeferredBEVBatch in both output modes,
+    equals the oracle's makeBEVMap(get_filtered_lidar(sweep)) flipped on the last axis where flip_w is
+    set (bit-exact in f64; the on-device float32 maps are those values rounded)."""
+    from data_process.kitti_dataloader import DeferredBEVBatch
+    from data_process.kitti_dataset import DeferredBEV
+    from sfa_hip import synthetic as syn
+    clouds = [syn.synthetic_point_cloud(300 + j)[:: 1 + j].copy() for j in range(3)]
+    flips = [True, False, True]
+    batch = DeferredBEVBatch([DeferredBEV(c, f) for c, f in zip(clouds, flips)])
+    host = batch.voxelize(gpu)
+    dev = batch.voxelize(gpu, on_device=True)
+    assert host.dtype == torch.float64 and host.device.type == "cpu"
+    assert dev.dtype == torch.float32 and dev.device == gpu
+    for i, (c, f) in enumerate(zip(clouds, flips)):
+        exp = bev_oracle.makeBEVMap(bev_oracle.get_filtered_lidar(c, gc.BOUNDARY), gc.BOUNDARY)
+        if f:
+            exp = exp[..., ::-1]
+        np.testing.assert_array_equal(host[i].numpy(), exp, err_msg=f"sweep {i} (flip {f})")
+        np.testing.assert_array_equal(dev[i].cpu().numpy(), exp.astype(np.float32), err_msg=f"sweep {i} on device")
