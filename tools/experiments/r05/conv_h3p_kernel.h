@@ -26,22 +26,9 @@
 
 namespace sfa {
 
-// n / d for 0 <= n < 2^31 by the round-up method with an add (Granlund-Montgomery):
-// q = (umulhi(n, m) + n) >> s, s = ceil(log2 d), m = floor(2^32 (2^s - d) / d) + 1 (< 2^32). Exact for
-// every d >= 1 and n < 2^31 (the 33-bit magic 2^32 + m is >= 2^(32+s) / d with error < d <= 2^s).
-struct FastDiv {
-  unsigned m;
-  int s;
-};
-inline FastDiv make_fastdiv(unsigned d) {
-  int s = 0;
-  while ((1ull << s) < d) ++s;
-  const unsigned long long m = ((1ull << 32) * ((1ull << s) - d)) / d + 1;
-  return FastDiv{(unsigned)m, s};
-}
-__device__ __forceinline__ int fdiv(int n, FastDiv f) {
-  return (int)((__umulhi((unsigned)n, f.m) + (unsigned)n) >> f.s);
-}
+// FastDiv / make_fast_div / fast_div: conv.h (the product's copy since round 5)
+inline FastDiv make_fastdiv(unsigned d) { return make_fast_div(d); }
+__device__ __forceinline__ int fdiv(int n, FastDiv f) { return fast_div(n, f); }
 
 struct H3pArgs {
   int units;      // m_tiles * n_tiles * nsplit
