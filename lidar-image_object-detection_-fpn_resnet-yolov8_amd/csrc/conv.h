@@ -219,8 +219,9 @@ struct ConvArgs {
   // FPN 1x1 convs: 1 = may run on the persistent weight-resident kernel (fpn_kernel.h), 0 = the
   // per-tile conv_h3 / conv_r3 kernels (model option SFA_OPT_FPN_GEMM)
   int fpn_gemm;
-  // multiply-high divisions by the input width / height (filled by the strip kernel's launch)
-  FastDiv fd_w, fd_h;
+  // multiply-high divisions by the input width / height (filled by the strip kernel's launch) and by
+  // the output width / height (conv_r3's)
+  FastDiv fd_w, fd_h, fd_ow, fd_oh;
 };
 
 // Bilinear x2 (align_corners) sample of a half-resolution NHWC tensor at output pixel

@@ -343,10 +343,10 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_h3_kerne
       oh = th * (BM / 16) + (loc >> 4);
       ow = ((tile - th * tw_n) << 4) + (loc & 15);
     } else {
-      ow = mm % a.OW;
-      const int t = mm / a.OW;
-      oh = t % a.OH;
-      b = t / a.OH;
+      const int t = fast_div(mm, a.fd_ow);  // round 5: multiply-high divisions (a.fd_ow / fd_oh)
+      ow = mm - t * a.OW;
+      b = fast_div(t, a.fd_oh);
+      oh = t - b * a.OH;
     }
 #pragma unroll
     for (int sg = 0; sg < NSEG; ++sg) {
@@ -378,12 +378,27 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_h3_kerne
     boff[j] = (int)(t * term_bytes) + (int)(((n0 + R) * wst + a.wk0 + 8 * lc) << 1);
   }
 
-  // fp16x3 scale of the frame of this lane's A row in each 32-row MFMA tile
+  // fp16x3 scale of the frame of this lane's A row in each 32-row MFMA tile: the block's first two
+  // frames' scales by uniform loads, rows of later frames (small maps) their own
   float as[TM], ainv[TM];
+  {
+    const int P = a.OH * a.OW, f0 = m0 / P, fb = (f0 + 1) * P;
+    float iA, iB;
+    const float sA = amax_frame_scale(a.amax_in, NSEG, f0, iA);
+    const float sB = fb < M ? amax_frame_scale(a.amax_in, NSEG, f0 + 1, iB) : (iB = iA, sA);
 #pragma unroll
-  for (int mi = 0; mi < TM; ++mi) {
-    const int m = min(m0 + wm * WM + mi * MT + (lane & (MT - 1)), M - 1);
-    as[mi] = amax_frame_scale(a.amax_in, NSEG, m / (a.OH * a.OW), ainv[mi]);
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = min(m0 + wm * WM + mi * MT + (lane & (MT - 1)), M - 1);
+      if (m < fb) {
+        as[mi] = sA;
+        ainv[mi] = iA;
+      } else if (m < fb + P) {
+        as[mi] = sB;
+        ainv[mi] = iB;
+      } else {
+        as[mi] = amax_frame_scale(a.amax_in, NSEG, m / P, ainv[mi]);
+      }
+    }
   }
 
   auto load_a = [&](auto sgc, const __amdgpu_buffer_rsrc_t rs, int kl, unsigned char* S) {
@@ -709,19 +724,22 @@ inline int launch_conv_h3_cfg(const ConvArgs& a, hipStream_t st) {
     set_error("conv_h3: bad grid (M=%d N=%d)", a.M, a.N);
     return SFA_E_INVALID;
   }
+  ConvArgs c = a;  // the row decomposition's multiply-high divisions
+  c.fd_ow = make_fast_div((unsigned)a.OW);
+  c.fd_oh = make_fast_div((unsigned)a.OH);
   if (a.res_up) {  // FPN skip convs (one segment): the instance with the upsampled-residual epilogue
     if (a.nseg != 1) {
       set_error("conv_h3: upsampled residual with two K-segments");
       return SFA_E_UNSUPPORTED;
     }
     hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 1, NMAJ, ABL, MF, WN, true>),
-                       dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WN) * 64), 0, st, a);
+                       dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WN) * 64), 0, st, c);
   } else if (a.nseg == 2) {
     hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 2, NMAJ, ABL, MF, WN>),
-                       dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WN) * 64), 0, st, a);
+                       dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WN) * 64), 0, st, c);
   } else {
     hipLaunchKernelGGL((conv_h3_kernel<BM, BN, WM, EPI, OCC, BK, NSTAGE, 1, NMAJ, ABL, MF, WN>),
-                       dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WN) * 64), 0, st, a);
+                       dim3((unsigned)nblocks), dim3((BM / WM) * (BN / WN) * 64), 0, st, c);
   }
   SFA_LAUNCH_CHECK();
   if (ks > 1) {  // the slices' partials combined by the reduce launch (element-strided partials: no tickets)

@@ -324,14 +324,15 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   const int M = a.M;
 
   // ---- A: this lane's rows (one per 16-row sub-tile), gather origins per segment ----
+  // (round 5: row decomposition by multiply-high divisions, a.fd_ow / a.fd_oh from the launch)
   int r_pix[NSEG][TM], r_ihw[NSEG][TM];
 #pragma unroll
   for (int mi = 0; mi < TM; ++mi) {
     const int m = m0 + wave * WM + mi * 16 + c16;
     const bool ok = m < M;
     const int mm = ok ? m : 0;
-    const int ow = mm % a.OW, t = mm / a.OW;
-    const int oh = t % a.OH, b = t / a.OH;
+    const int t = fast_div(mm, a.fd_ow), ow = mm - t * a.OW;
+    const int b = fast_div(t, a.fd_oh), oh = t - b * a.OH;
 #pragma unroll
     for (int sg = 0; sg < NSEG; ++sg) {
       const ConvSeg& sgm = a.seg[sg];
@@ -363,13 +364,21 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
     boff_s[j] = (int)((e / ND_BT) * term_bytes) + (e % ND_BT) * 16 * wst * 2;  // uniform: wave, j, args
   }
 
-  // fp16x3 scale of the frame of this lane's A row in each 16-row sub-tile
+  // fp16x3 scale of the frame of this lane's A row in each 16-row sub-tile: the block's first two
+  // frames' scales by uniform loads, rows of later frames (small maps) their own
   float as[TM];  // 1 / as (exact: powers of two) is recomputed for the epilogue
-#pragma unroll
-  for (int mi = 0; mi < TM; ++mi) {
-    const int m = min(m0 + wave * WM + mi * 16 + c16, M - 1);
+  {
+    const int P = a.OH * a.OW, f0 = m0 / P, fb = (f0 + 1) * P;
     float sinv;
-    as[mi] = amax_frame_scale(a.amax_in, NSEG, m / (a.OH * a.OW), sinv);
+    const float sA = amax_frame_scale(a.amax_in, NSEG, f0, sinv);
+    const float sB = fb < M ? amax_frame_scale(a.amax_in, NSEG, f0 + 1, sinv) : sA;
+#pragma unroll
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = min(m0 + wave * WM + mi * 16 + c16, M - 1);
+      if (m < fb) as[mi] = sA;
+      else if (m < fb + P) as[mi] = sB;
+      else as[mi] = amax_frame_scale(a.amax_in, NSEG, m / P, sinv);
+    }
   }
 
   r3_u32x4 raw[TM][2];  // A fragment of the next K-tile (f32 bits)
@@ -708,12 +717,15 @@ inline int launch_conv_r3_cfg(const ConvArgs& a, hipStream_t st) {
     set_error("conv_r3: bad grid (M=%d N=%d)", a.M, a.N);
     return SFA_E_INVALID;
   }
+  ConvArgs b = a;  // the row decomposition's multiply-high divisions
+  b.fd_ow = make_fast_div((unsigned)a.OW);
+  b.fd_oh = make_fast_div((unsigned)a.OH);
   if (a.nseg == 2)
     hipLaunchKernelGGL((conv_r3_kernel<BM, BN, WM, EPI, OCC, NSTAGE, 2, ABL>), dim3((unsigned)nblocks),
-                       dim3((BM / WM) * 64), 0, st, a);
+                       dim3((BM / WM) * 64), 0, st, b);
   else
     hipLaunchKernelGGL((conv_r3_kernel<BM, BN, WM, EPI, OCC, NSTAGE, 1, ABL>), dim3((unsigned)nblocks),
-                       dim3((BM / WM) * 64), 0, st, a);
+                       dim3((BM / WM) * 64), 0, st, b);
   SFA_LAUNCH_CHECK();
   if (ks > 1) {  // the slices' partials combined by the reduce launch
     const long long nel = (long long)a.M * a.N;

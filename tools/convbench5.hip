@@ -177,18 +177,21 @@ int main(int argc, char** argv) {
   std::vector<Shape> shapes = {
       {"layer1 3x3 64->64 +res", 16, 152, 152, 64, 64, true},
       {"layer2 3x3 128->128", 16, 76, 76, 128, 128, false},
+      {"layer2 3x3 128->128 +res", 16, 76, 76, 128, 128, true},
       {"layer3 3x3 256->256", 16, 38, 38, 256, 256, false},
+      {"layer3 3x3 256->256 +res", 16, 38, 38, 256, 256, true},
       {"layer4 3x3 512->512", 16, 19, 19, 512, 512, false},
   };
-  std::vector<Cand> l1 = {CS(128, 64, 32, 3, 142, 1), CP(128, 64, 32, 3, false, 1), CS(128, 64, 32, 3, 142, 1),
-                          CP(128, 64, 32, 3, false, 1)};
-  std::vector<Cand> l2 = {CS(128, 128, 32, 2, 10, 1), CP(128, 128, 32, 2, false, 1), CS(128, 128, 32, 2, 10, 1),
-                          CP(128, 128, 32, 2, false, 1)};
+  // round 5: 64 x 64 tiles at 4 blocks / CU (4 waves per SIMD) against the product 128 x 64 at 3
+  std::vector<Cand> l1 = {CS(128, 64, 32, 3, 142, 1), CS(64, 64, 16, 4, 142, 1), CS(64, 64, 16, 4, 14, 1),
+                          CS(128, 64, 32, 3, 142, 1), CS(64, 64, 16, 4, 142, 1)};
+  // round 5: the pre-split strip (4) and the residual prefetch (128) on the 128-wide tiles
+  std::vector<Cand> l2 = {CS(128, 128, 32, 2, 10, 1), CS(128, 128, 32, 2, 14, 1), CS(128, 128, 32, 2, 142, 1),
+                          CS(128, 128, 32, 2, 10, 1), CS(128, 128, 32, 2, 14, 1), CS(128, 128, 32, 2, 142, 1)};
   // round 5: the heads' register-A kernel (half-tile stagger, 3-stage W ring) on 256-wide tiles, the
   // grid filled by split-K (reduce launch)
-  std::vector<Cand> l3 = {CS(64, 128, 16, 3, 10, 1), CR(192, 256, 32, 1, 3, 1603844, 2), CR(256, 256, 32, 1, 3, 1603844, 2),
-                          CR(256, 256, 32, 1, 3, 1603844, 3), CR(192, 256, 32, 1, 3, 1603844, 3),
-                          CS(64, 128, 16, 3, 10, 1), CR(192, 256, 32, 1, 3, 1603844, 2)};
+  std::vector<Cand> l3 = {CS(64, 128, 16, 3, 10, 1), CS(64, 128, 16, 3, 14, 1), CS(64, 128, 16, 3, 142, 1),
+                          CS(64, 128, 16, 3, 10, 1), CS(64, 128, 16, 3, 14, 1), CS(64, 128, 16, 3, 142, 1)};
   std::vector<Cand> l4 = {CS(128, 64, 32, 3, 142, 2), CT(128, 64, 32, 3, 142, 2), CR(192, 256, 32, 1, 3, 1603844, 4),
                           CR(256, 256, 32, 1, 3, 1603844, 6), CR(192, 256, 32, 1, 3, 1603844, 3),
                           CS(128, 64, 32, 3, 142, 2), CT(128, 64, 32, 3, 142, 2), CR(192, 256, 32, 1, 3, 1603844, 4)};
