@@ -84,10 +84,12 @@ constexpr int R3_FPN = 256 | 2048 | 32768;
 // with three W stages (1048576: -4.6 / -3.1 / -1.0 % per launch on L1 / L2 / L0, bit-identical,
 // profiles/r03h_convbench_heads_stagger.txt)
 constexpr int R3_HEAD_STAG = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536 | 524288 | 1048576;
-// strip kernel (conv_h3s_kernel.h bits): transposed epilogue (2) and v_fma_mix split (8); the
-// 64-wide also the pre-split strip (4) and the residual tile loaded during the last super-step (128)
+// strip kernel (conv_h3s_kernel.h bits): transposed epilogue (2), v_fma_mix split (8), the pre-split
+// strip (4) and the residual tile loaded during the last super-step (128) on every tile shape (round
+// 5: with the one-latency presplit the 128-wide tiles gain from them too, layer2 -4.6 % / -6.5 % with a
+// residual, layer3 -1 / -2 %, bit-identical: profiles/r05j_*; the names of the former two forms stay)
 constexpr int H3S_64 = 2 | 4 | 8 | 128;
-constexpr int H3S_128 = 2 | 8;
+constexpr int H3S_128 = 2 | 4 | 8 | 128;
 
 // FPN 1x1 convs (commuted: the low-resolution W_a . x and the skip conv with the upsampled
 // residual) on the persistent weight-resident kernel (fpn_kernel.h), by channel count.

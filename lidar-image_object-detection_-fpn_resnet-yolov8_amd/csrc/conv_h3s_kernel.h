@@ -55,7 +55,8 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
   constexpr int PR_BYTES = (PROWS + 1) * 64;  // per term: 32 fp16 per row, + one zero row
   constexpr int NSB = PS ? 1 : 2;             // f32 strip buffers
   constexpr int MAIN_BYTES = NSB * S_BYTES + 2 * W_BYTES + (PS ? NW * 2 * PR_BYTES : 0);
-  constexpr int LDS_BYTES = MAIN_BYTES;
+  constexpr int CSB_OFF = MAIN_BYTES;  // the tile's winv / bias columns (epilogue), staged in the prologue
+  constexpr int LDS_BYTES = MAIN_BYTES + 2 * BN * 4;
   static_assert(NW % 2 == 0 && WM % 16 == 0 && BN % 16 == 0, "tile");
   static_assert((ABL & 10) == 10 && (ABL & ~(2 | 4 | 8 | 128 | 256)) == 0, "product strip-kernel form (see the bit list)");
   static_assert(EPI == EPI_STD, "transposed form: standard epilogue only");
@@ -228,6 +229,11 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
       }
     }
   };
+  // the epilogue's winv / bias columns: loaded here, written to LDS after the first k-step (their
+  // latency hidden by it), read after the K loop's later barriers
+  float* const CSB = reinterpret_cast<float*>(smem + CSB_OFF);
+  static_assert(2 * BN <= NT, "one winv / bias value per thread");
+  const float csb_v = tid < BN ? a.winv[n0 + tid] : (tid < 2 * BN && a.bias ? a.bias[n0 + tid - BN] : 0.f);
   if constexpr (PS) {  // the zero rows (conv padding at kw 0 / 2)
     if (lane < 8) *reinterpret_cast<x6_f32x4*>(PH + (lane & 4 ? PR_BYTES : 0) + PROWS * 64 + (lane & 3) * 16) =
         x6_f32x4{0.f, 0.f, 0.f, 0.f};
@@ -329,6 +335,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
         }
         if (kw == 0) presplit(smem);
         compute(smem, WB + (t & 1) * W_BYTES, kw);
+        if (t == 0 && tid < 2 * BN) CSB[tid] = csb_v;
         if constexpr (RW) {
           if (RESPF && last && kw == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           else wait_w_regs(strip_after ? 1 : 0);
@@ -353,6 +360,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
       else load_w(wnext, wdst);
       if (kw == 0) load_strip(last ? s : s + 1, sdst);
       compute(smem + (sl & 1) * S_BYTES, WB + (t & 1) * W_BYTES, kw);
+      if (t == 0 && tid < 2 * BN) CSB[tid] = csb_v;
       if constexpr (RW) {
         wait_w_regs(kw == 0 ? 1 : 0);
         store_w_regs(wdst);
@@ -412,7 +420,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     return;
   }
   __syncthreads();
-  r3t_epilogue_std<TM, TN, NT, false, RESPF>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv, rvp);
+  r3t_epilogue_std<TM, TN, NT, false, RESPF, true>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv, rvp, CSB);
 }
 
 template <int BM, int BN, int WM, int EPI, int OCC, int ABL = 0>

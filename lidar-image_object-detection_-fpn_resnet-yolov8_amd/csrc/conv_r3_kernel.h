@@ -55,11 +55,13 @@ __device__ __forceinline__ void r3t_res_load(const ConvArgs& a, x6_f32x4 (&rv)[T
 }
 
 // PRE: the residual tile (a.res) was loaded by the caller (r3t_res_load) into `pre`, so its
-// latency hid behind the MFMAs.
-template <int TM, int TN, int NT, bool RU = false, bool PRE = false>
+// latency hid behind the MFMAs. CSL: the block's winv / bias columns n0 .. were staged in LDS by the
+// caller (csb: [TN * 16] winv, then [TN * 16] bias, 0 without a bias) instead of read from global
+// memory here (round 5: their latency was exposed at the end of every tile).
+template <int TM, int TN, int NT, bool RU = false, bool PRE = false, bool CSL = false>
 __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
                                                  int mrow0, int m0, int n0, int lane, const float (&ainv)[TM],
-                                                 const x6_f32x4 (*pre)[TN] = nullptr) {
+                                                 const x6_f32x4 (*pre)[TN] = nullptr, const float* csb = nullptr) {
   // every element is evaluated by the same rounding sequence (explicit fmaf, no contraction):
   // left to the compiler, the unrolled copies were contracted differently (some mul + add, some
   // fma, some packed), so a pixel's value depended on its row within the tile, i.e. on the
@@ -107,8 +109,14 @@ __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&ac
 #pragma unroll
   for (int ni = 0; ni < TN; ++ni) {
     const int n = n0 + ni * 16 + 4 * g;
-    const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(a.winv + n);
-    const x6_f32x4 bn = a.bias ? *reinterpret_cast<const x6_f32x4*>(a.bias + n) : x6_f32x4{0.f, 0.f, 0.f, 0.f};
+    x6_f32x4 cs, bn;
+    if constexpr (CSL) {
+      cs = *reinterpret_cast<const x6_f32x4*>(csb + ni * 16 + 4 * g);
+      bn = *reinterpret_cast<const x6_f32x4*>(csb + TN * 16 + ni * 16 + 4 * g);
+    } else {
+      cs = *reinterpret_cast<const x6_f32x4*>(a.winv + n);
+      bn = a.bias ? *reinterpret_cast<const x6_f32x4*>(a.bias + n) : x6_f32x4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
       const int m = mrow0 + mi * 16 + c16;
