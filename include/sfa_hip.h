@@ -173,9 +173,10 @@ int sfa_model_get_math(const sfa_model* model);
  *   SFA_OPT_FPN_COMMUTE (SFA_FPN_COMMUTE) bit mask of the FPN levels run commuted (7, fp16x3)
  *   SFA_OPT_FPN_GEMM    (SFA_FPN_GEMM)    bit mask of the commuted FPN 1x1 convs on the persistent
  *                                         weight-resident kernel: bit f = level f's low-resolution
- *                                         conv, bit 3 + f = its skip conv (37: the low-res convs of
- *                                         levels 0 and 2, the level-2 skip conv on full rows); the
- *                                         others on the per-tile kernels
+ *                                         conv, bit 3 + f = its skip conv (61: the low-res convs of
+ *                                         levels 0 and 2, the level-2 skip conv on full rows, the
+ *                                         level-0 / 1 skip convs on flat pixel steps); the others on
+ *                                         the per-tile kernels
  *   SFA_OPT_SPLITK_TICKETS (SFA_SPLITK_TICKETS) 1 (default): the split-K layer4 strip convs combine
  *                                         their slices in the conv kernel (the last slice of a tile to
  *                                         finish, by an atomic ticket); 0: a reduce launch per conv; the

@@ -96,6 +96,11 @@ constexpr int H3S_128 = 2 | 4 | 8 | 128;
 static int launch_fpn(const ConvArgs& a, hipStream_t st) {
   const int C = a.seg[0].C;
   if (a.res_up) {
+    if (a.OW <= 2 * fpn_seg::WHMAX) {  // narrow levels: flat pixel steps, the taps from an LDS row ring
+      const int rc = C == 128 ? launch_fpn_seg_cfg<128, 1>(a, st) : C == 256 ? launch_fpn_seg_cfg<256, 1>(a, st)
+                                                                             : SFA_E_UNSUPPORTED;
+      if (rc != SFA_E_UNSUPPORTED) return rc;
+    }
     {  // full rows, the bilinear taps from an LDS ring of source rows
       const int rc = launch_fpn_row(a, st);
       if (rc != SFA_E_UNSUPPORTED) return rc;

@@ -383,9 +383,12 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_h3_kerne
   float as[TM], ainv[TM];
   {
     const int P = a.OH * a.OW, f0 = m0 / P, fb = (f0 + 1) * P;
-    float iA, iB;
-    const float sA = amax_frame_scale(a.amax_in, NSEG, f0, iA);
-    const float sB = fb < M ? amax_frame_scale(a.amax_in, NSEG, f0 + 1, iB) : (iB = iA, sA);
+    float sA, iA, sB, iB;
+    amax_frame_scale2(a.amax_in, NSEG, f0, min(f0 + 1, (M - 1) / P), sA, iA, sB, iB);
+    if (fb >= M) {
+      sB = sA;
+      iB = iA;
+    }
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
       const int m = min(m0 + wm * WM + mi * MT + (lane & (MT - 1)), M - 1);

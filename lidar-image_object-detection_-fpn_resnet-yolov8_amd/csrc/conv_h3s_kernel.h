@@ -112,32 +112,6 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     const int lc = (lane & 3) ^ swzB(R);
     boff[jj] = (int)(term * term_bytes) + (int)(((n0 + R) * a.Kpad + 8 * lc) << 1);
   }
-  // the fp16x3 scales of the block's first two frames (uniform loads); x of this lane's A row in each
-  // 16-row tile (kw edge masks) and its frame's scale — rows of later frames (blocks taller than a
-  // frame: small maps) read their own
-  const int P = a.OH * a.OW;
-  const int f0 = m0 / P;
-  const int fb = (f0 + 1) * P;  // first row of the next frame
-  float iA, iB;
-  const float sA = amax_frame_scale(a.amax_in, 1, f0, iA);
-  const float sB = fb < M ? amax_frame_scale(a.amax_in, 1, f0 + 1, iB) : (iB = iA, sA);
-  const int c16 = lane & 15, gq = lane >> 4;
-  int xm[TM];
-  float as[TM], ainv[TM];
-#pragma unroll
-  for (int mi = 0; mi < TM; ++mi) {
-    const int m = min(m0 + wave * WM + mi * 16 + c16, M - 1);
-    xm[mi] = m - fast_div(m, a.fd_w) * W;
-    if (m < fb) {
-      as[mi] = sA;
-      ainv[mi] = iA;
-    } else if (m < fb + P) {
-      as[mi] = sB;
-      ainv[mi] = iB;
-    } else {
-      as[mi] = amax_frame_scale(a.amax_in, 1, m / P, ainv[mi]);
-    }
-  }
   auto swzP = [](int R) { return ((R >> 2) & 1) << 1; };  // conflict-free at every kw row offset
 
   const int lognchunk = g.logC - 5, nchunk = 1 << lognchunk;
@@ -165,6 +139,36 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
             (unsigned)(boff[jj] + 2 * k0), 0, 0, 0);
     }
   };
+  // the fp16x3 scales of the block's first two frames (uniform loads); x of this lane's A row in each
+  // 16-row tile (kw edge masks) and its frame's scale — rows of later frames (blocks taller than a
+  // frame: small maps) read their own
+  const int P = a.OH * a.OW;
+  const int f0 = m0 / P;
+  const int fb = (f0 + 1) * P;  // first row of the next frame
+  // both frames' words loaded at once (the second frame clamped into the batch; used only if it exists)
+  float sA, iA, sB, iB;
+  amax_frame_scale2(a.amax_in, 1, f0, min(f0 + 1, (M - 1) / P), sA, iA, sB, iB);
+  if (fb >= M) {
+    sB = sA;
+    iB = iA;
+  }
+  const int c16 = lane & 15, gq = lane >> 4;
+  int xm[TM];
+  float as[TM], ainv[TM];
+#pragma unroll
+  for (int mi = 0; mi < TM; ++mi) {
+    const int m = min(m0 + wave * WM + mi * 16 + c16, M - 1);
+    xm[mi] = m - fast_div(m, a.fd_w) * W;
+    if (m < fb) {
+      as[mi] = sA;
+      ainv[mi] = iA;
+    } else if (m < fb + P) {
+      as[mi] = sB;
+      ainv[mi] = iB;
+    } else {
+      as[mi] = amax_frame_scale(a.amax_in, 1, m / P, ainv[mi]);
+    }
+  }
   x6_u32x4 wreg[NB];  // RW: the next k-step's W pieces
   auto load_w_regs = [&](int k0) {
 #pragma unroll

@@ -377,9 +377,9 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   float as[TM];  // 1 / as (exact: powers of two) is recomputed for the epilogue
   {
     const int P = a.OH * a.OW, f0 = m0 / P, fb = (f0 + 1) * P;
-    float sinv;
-    const float sA = amax_frame_scale(a.amax_in, NSEG, f0, sinv);
-    const float sB = fb < M ? amax_frame_scale(a.amax_in, NSEG, f0 + 1, sinv) : sA;
+    float sinv, sA, sB;
+    amax_frame_scale2(a.amax_in, NSEG, f0, min(f0 + 1, (M - 1) / P), sA, sinv, sB, sinv);
+    if (fb >= M) sB = sA;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
       const int m = min(m0 + wave * WM + mi * 16 + c16, M - 1);

@@ -115,6 +115,34 @@ __device__ __forceinline__ void fpn_epilogue(const ConvArgs& a, f32x4_t (&acc)[T
   if (a.amax_out) amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1, reinterpret_cast<float*>(red));
 }
 
+// The fp16x3 weight slice of an FPN kernel (columns n0 .. n0 + NBC - 1, KT K-tiles from column wk0 of
+// the [2 terms][N][wstride] packed weights) into LDS in conv_r3's swizzled fragment layout
+// [kt][term][n][16-B slot q ^ swzB(n)] (rows of 64 B, contiguous), by LDS-DMA: slot s of the region
+// takes (kt, term, n, q = (s & 3) ^ swzB(n)), every piece in flight at once.  The element-wise
+// load -> ds_write loop it replaces (round 5) waited one memory latency per iteration: 4 .. 32
+// serialised round trips per block.  The caller waits (vmcnt(0) + barrier) before reading it.
+template <int KT, int NBC, int NW>
+__device__ __forceinline__ void fpn_stage_w(const ConvArgs& a, int n0, unsigned char* smem, int wave, int lane) {
+  constexpr int PIECES = KT * 2 * NBC * 4 / 64;  // 64 slots of 16 B per piece
+  static_assert((KT * 2 * NBC * 4) % 64 == 0, "whole pieces");
+  const int wst = a.wstride ? a.wstride : a.Kpad;
+  const size_t term_elems = (size_t)a.N * wst;
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.wh), (short)0,
+                                                                       (int)(term_elems * 2 * 2), 0x00020000);
+  auto swzB = [](int R) { return ((R >> 2) & 3) ^ ((((R & 15) + 4) >> 3) & 1); };
+#pragma unroll
+  for (int i = 0; i < (PIECES + NW - 1) / NW; ++i) {
+    const int pc = wave + NW * i;
+    if (pc >= PIECES) break;  // wave-uniform
+    const int sl = pc * 64 + lane;
+    const int n = (sl >> 2) % NBC, r2 = (sl >> 2) / NBC, term = r2 & 1, kt = r2 >> 1;
+    const int q = (sl & 3) ^ swzB(n);
+    const unsigned off = (unsigned)((term * term_elems + (size_t)(n0 + n) * wst + a.wk0 + kt * 32 + 8 * q) * 2);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(smem + pc * 1024), 16, off,
+                                             0, 0, 0);
+  }
+}
+
 template <int K, int BN, bool RU, int OCC>
 __global__ void __launch_bounds__(256, OCC) fpn_gemm_kernel(const ConvArgs a, int n_mt) {
   using G = FpnGeom<K, BN, RU, OCC>;
@@ -135,20 +163,12 @@ __global__ void __launch_bounds__(256, OCC) fpn_gemm_kernel(const ConvArgs a, in
   const int M = a.M, P = a.OH * a.OW, nframes = (M + P - 1) / P;
 
   // the weight slice (columns n0 .. n0 + BN - 1, K columns from wk0) and the frame scales -> LDS
-  {
-    const int wst = a.wstride ? a.wstride : a.Kpad;
-    const size_t term_elems = (size_t)a.N * wst;
-    for (int c = tid; c < G::KT * 2 * BN * 4; c += NT) {
-      const int q = c & 3, n = (c >> 2) % BN, rest = (c >> 2) / BN, term = rest & 1, kt = rest >> 1;
-      const r3_u32x4 v = *reinterpret_cast<const r3_u32x4*>(a.wh + term * term_elems + (size_t)(n0 + n) * wst + a.wk0 +
-                                                           kt * 32 + 8 * q);
-      *reinterpret_cast<r3_u32x4*>(smem + kt * STAGE + term * TERM_B + n * BROW + ((q ^ swzB(n)) << 4)) = v;
-    }
-    for (int f = tid; f < nframes; f += NT) {
-      float sinv;
-      FS[f] = amax_frame_scale(a.amax_in, 1, f, sinv);
-    }
+  fpn_stage_w<G::KT, BN, NW>(a, n0, smem, wave, lane);
+  for (int f = tid; f < nframes; f += NT) {
+    float sinv;
+    FS[f] = amax_frame_scale(a.amax_in, 1, f, sinv);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.seg[0].x), (short)0,
@@ -326,19 +346,11 @@ __global__ void __launch_bounds__(256, OCC) fpn_row_kernel(const ConvArgs a, int
   if (y1 <= y0) return;  // uniform per block
 
   // the weight slice (columns n0 .., K columns from wk0) in conv_r3's swizzled fragment layout
-  {
-    const int wst = a.wstride ? a.wstride : a.Kpad;
-    const size_t term_elems = (size_t)N * wst;
-    for (int c = tid; c < KT * 2 * NB * 4; c += NT) {
-      const int q = c & 3, n = (c >> 2) % NB, r2 = (c >> 2) / NB, term = r2 & 1, kt = r2 >> 1;
-      const r3_u32x4 v = *reinterpret_cast<const r3_u32x4*>(a.wh + term * term_elems + (size_t)(n0 + n) * wst + a.wk0 +
-                                                           kt * 32 + 8 * q);
-      *reinterpret_cast<r3_u32x4*>(smem + kt * STAGE + term * TERM_B + n * BROW + ((q ^ swzB(n)) << 4)) = v;
-    }
-  }
-  for (int i = tid; i < NB; i += NT) {
-    CSB[i] = a.winv[n0 + i];
-    CSB[NB + i] = a.bias ? a.bias[n0 + i] : 0.f;
+  fpn_stage_w<KT, NB, NW>(a, n0, smem, wave, lane);
+  if (tid < NB) {  // both loads in flight before either store (NB <= NT)
+    const float wv = a.winv[n0 + tid], bv = a.bias ? a.bias[n0 + tid] : 0.f;
+    CSB[tid] = wv;
+    CSB[NB + tid] = bv;
   }
   float ainv;
   const float as = amax_frame_scale(a.amax_in, 1, b, ainv);
@@ -500,6 +512,227 @@ inline int launch_fpn_row_cfg(const ConvArgs& a, hipStream_t st) {
   int segs = (OCC * ncu + frames * nct - 1) / (frames * nct);  // about OCC blocks per CU
   segs = segs < 1 ? 1 : (segs > a.OH ? a.OH : segs);
   hipLaunchKernelGGL((fpn_row_kernel<K, RB, OCC>), dim3((unsigned)(frames * segs * nct)), dim3(NT), 0, st, a, segs);
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
+// FPN skip convs of the narrow levels (round 5): fpn_row_kernel walks one output
+// row per step, which at 76 / 38 pixels is 2.4 - 4.75 row blocks of 16 for 4 waves, a barrier and an
+// exposed load latency per row (profiles/r04m_*: slower than conv_r3 there).  Here a block walks its
+// frame segment as a FLAT pixel range in steps of 16 NW pixels (one 16-pixel block per wave, rows
+// crossed freely): every wave has work each step and a step covers 1.7 - 3.4 output rows.  The
+// half-resolution source rows of the residual taps live in an LDS ring of NSLOT rows (row r in slot
+// r % NSLOT), the rows the next step needs loaded by LDS-DMA during this one; each lane finds its own
+// pixel's (y, x), tap rows and weights.  Weight slice, scales / biases in LDS and the next step's A
+// fragments issued before this step's MFMAs, as fpn_row_kernel; products, K order, split and the
+// epilogue's rounding sequence are conv_r3_kernel's (R3_FPN): the same bits.
+namespace fpn_seg {
+constexpr int NW = 8, NT = 64 * NW, NB = 64, TNB = NB / 16, P = 16 * NW;  // pixels per step
+constexpr int BROW = 64, TERM_B = NB * BROW, STAGE = 2 * TERM_B;
+constexpr int WHMAX = 40, NSLOT = 8, SLOT = WHMAX * NB * 4;  // source rows of <= 40 pixels
+__host__ __device__ constexpr int lds_bytes(int K) { return (K / 32) * STAGE + NSLOT * SLOT + 2 * NB * 4 + NW * 4; }
+// the source rows one step (pixels [p, p + P) of rows y0 .. y1 - 1) reads: [lo, hi]
+__host__ __device__ inline void step_rows(int p, int pend, int W, int Hh, float sh, int& lo, int& hi) {
+  const int ya = p / W, yb = (min(p + P, pend) - 1) / W;
+  lo = (int)(sh * (float)ya);
+  hi = min((int)(sh * (float)yb) + 1, Hh - 1);
+}
+}  // namespace fpn_seg
+
+template <int K, int OCC>
+__global__ void __launch_bounds__(fpn_seg::NT, OCC) fpn_seg_kernel(const ConvArgs a, int segs) {
+#pragma clang fp contract(off)
+  using namespace fpn_seg;
+  constexpr int KT = K / 32, W_BYTES = KT * STAGE;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[lds_bytes(K)];
+  unsigned char* const ring = smem + W_BYTES;
+  float* const CSB = reinterpret_cast<float*>(smem + W_BYTES + NSLOT * SLOT);  // [NB] winv, [NB] bias
+  float* const red = CSB + 2 * NB;
+  auto swzB = [](int R) { return ((R >> 2) & 3) ^ ((((R & 15) + 4) >> 3) & 1); };
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int c16 = lane & 15, g = lane >> 4;
+  const int H = a.OH, W = a.OW, Hh = H >> 1, Wh = W >> 1, N = a.N;
+  const int nct = N / NB;
+  const int ct = blockIdx.x % nct, rest = blockIdx.x / nct;
+  const int b = rest / segs, sk = rest - b * segs;
+  const int n0 = ct * NB;
+  const int pbeg = (sk * H / segs) * W, pend = ((sk + 1) * H / segs) * W;  // the segment's pixels
+  if (pend <= pbeg) return;  // uniform per block
+
+  // the weight slice (columns n0 .., K columns from wk0) in conv_r3's swizzled fragment layout
+  fpn_stage_w<KT, NB, NW>(a, n0, smem, wave, lane);
+  if (tid < NB) {  // both loads in flight before either store (NB <= NT)
+    const float wv = a.winv[n0 + tid], bv = a.bias ? a.bias[n0 + tid] : 0.f;
+    CSB[tid] = wv;
+    CSB[NB + tid] = bv;
+  }
+  float ainv;
+  const float as = amax_frame_scale(a.amax_in, 1, b, ainv);
+  ainv = 1.f / as;  // as conv_r3 forms it
+
+  // source rows (half resolution): the block's NB channels of each pixel by LDS-DMA (16 B per lane,
+  // LDS in item order = [pixel][NB channels]); the pieces of consecutive rows spread over the waves
+  const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.res_up), (short)0, (int)((size_t)(a.M / (H * W)) * Hh * Wh * N * 4), 0x00020000);
+  const int items = Wh * (NB / 4), npc = (items + 63) >> 6;
+  auto dma_rows = [&](int r0, int r1) {  // rows r0 .. r1
+    for (int u = wave; u < (r1 - r0 + 1) * npc; u += NW) {
+      const int sy = r0 + u / npc, piece = u - (u / npc) * npc;
+      const int it = piece * 64 + lane;
+      const size_t rbase = ((size_t)(b * Hh + sy) * Wh) * N + n0;  // floats
+      const unsigned off = it < items ? (unsigned)((rbase + (size_t)(it / (NB / 4)) * N + 4 * (it % (NB / 4))) * 4) : 0x80000000u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsr, (__attribute__((address_space(3))) void*)(ring + (sy % NSLOT) * SLOT + piece * 1024), 16, off, 0, 0, 0);
+    }
+  };
+
+  // A: lane (c16, g) -> pixel p + 16 wave + c16 of the frame, channels 32 kt + 8 g .. + 7
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.seg[0].x), (short)0,
+                                                                       (int)a.seg[0].bytes, 0x00020000);
+  const size_t fpix = (size_t)b * H * W;  // the frame's first pixel
+  r3_u32x4 ra[KT][2];
+  auto load_a = [&](int p) {
+    const int q = p + 16 * wave + c16;
+    const bool ok = q < pend;
+    const unsigned base = ok ? (unsigned)(((fpix + q) * K + 8 * g) * 4) : 0x80000000u;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const unsigned off = ok ? base + kt * 128u : base;
+      ra[kt][0] = __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0);
+      ra[kt][1] = __builtin_amdgcn_raw_buffer_load_b128(rsx, off + 16u, 0, 0);
+    }
+  };
+
+  // prologue: the first step's source rows and A fragments
+  int lo, hi;
+  step_rows(pbeg, pend, W, Hh, a.res_sh, lo, hi);
+  dma_rows(lo, hi);
+  load_a(pbeg);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int bfo = c16 * BROW + ((g ^ swzB(c16)) << 4);
+  float tmx = 0.f;
+  for (int p = pbeg; p < pend; p += P) {
+    const bool more = p + P < pend;
+    // the rows the next step needs beyond this one's (slots of rows below this step's lowest: free)
+    if (more) {
+      int lo2, hi2;
+      step_rows(p + P, pend, W, Hh, a.res_sh, lo2, hi2);
+      if (hi2 > hi) dma_rows(max(hi + 1, lo2), hi2);
+      hi = hi2;
+    }
+    // this step's A split into fp16 terms first, so the next step's loads go out before the MFMAs
+    f16x8_t hf[KT][2];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+      split2h_x8(__builtin_bit_cast(x6_f32x4, ra[kt][0]), __builtin_bit_cast(x6_f32x4, ra[kt][1]), as, hf[kt][0],
+                 hf[kt][1]);
+    if (more) load_a(p + P);
+    f32x4_t acc[TNB];
+#pragma unroll
+    for (int ni = 0; ni < TNB; ++ni) acc[ni] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const unsigned char* S = smem + kt * STAGE;
+#pragma unroll
+      for (int ni = 0; ni < TNB; ++ni) {
+        const f16x8_t c0 = *reinterpret_cast<const f16x8_t*>(S + bfo + ni * 16 * BROW);
+        const f16x8_t c1 = *reinterpret_cast<const f16x8_t*>(S + TERM_B + bfo + ni * 16 * BROW);
+        f32x4_t cc = acc[ni];
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[kt][1], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c1, hf[kt][0], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(c0, hf[kt][0], cc, 0, 0, 0);
+        acc[ni] = cc;
+      }
+    }
+    // epilogue (r3t_epilogue_std with the upsampled residual): this lane's pixel, taps from the ring
+    const int q = p + 16 * wave + c16;
+    const bool in = q < pend;
+    const int y = in ? q / W : 0, x = in ? q - y * W : 0;
+    const float fy = a.res_sh * (float)y;
+    const int sy0 = (int)fy, sy1 = sy0 + (sy0 < Hh - 1 ? 1 : 0);
+    const float ly1 = fy - (float)sy0, ly0 = 1.f - ly1;
+    const float fx = a.res_sw * (float)x;
+    const int sx0 = (int)fx, sx1 = sx0 + (sx0 < Wh - 1 ? 1 : 0);
+    const float lx1 = fx - (float)sx0, lx0 = 1.f - lx1;
+    const unsigned char* R0 = ring + (sy0 % NSLOT) * SLOT;
+    const unsigned char* R1 = ring + (sy1 % NSLOT) * SLOT;
+    const int o0 = sx0 * NB * 4, o1 = sx1 * NB * 4;
+#pragma unroll
+    for (int ni = 0; ni < TNB; ++ni) {
+      const int n = ni * 16 + 4 * g;
+      const x6_f32x4 a00 = *reinterpret_cast<const x6_f32x4*>(R0 + o0 + n * 4);
+      const x6_f32x4 a01 = *reinterpret_cast<const x6_f32x4*>(R0 + o1 + n * 4);
+      const x6_f32x4 a10 = *reinterpret_cast<const x6_f32x4*>(R1 + o0 + n * 4);
+      const x6_f32x4 a11 = *reinterpret_cast<const x6_f32x4*>(R1 + o1 + n * 4);
+      const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(CSB + n);
+      const x6_f32x4 bn = *reinterpret_cast<const x6_f32x4*>(CSB + NB + n);
+      x6_f32x4 val;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float rv = fmaf(ly0, fmaf(lx0, a00[v], lx1 * a01[v]), ly1 * fmaf(lx0, a10[v], lx1 * a11[v]));
+        float t = fmaf(acc[ni][v] * ainv, cs[v], bn[v]);
+        t += rv;
+        if (a.relu) t = fmaxf(t, 0.f);
+        val[v] = t;
+      }
+      if (in) {
+        *reinterpret_cast<x6_f32x4*>(a.y + (fpix + q) * N + n0 + n) = val;
+        tmx = fmaxf(tmx, fmaxf(fmaxf(fabsf(val[0]), fabsf(val[1])), fmaxf(fabsf(val[2]), fabsf(val[3]))));
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next step's A and this wave's DMA pieces
+    __syncthreads();  // the ring rows written above are visible; every wave is done with this step's taps
+  }
+  if (a.amax_out) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) tmx = fmaxf(tmx, __shfl_xor(tmx, o, 64));
+    if (lane == 0) red[wave] = tmx;
+    __syncthreads();
+    if (tid == 0) {
+      float m = red[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) m = fmaxf(m, red[w]);
+      if (m > 0.f) amax_atomic(a.amax_out, b, m);
+    }
+  }
+}
+
+// An FPN skip conv on flat pixel steps: K = C 128 / 256, N a multiple of 64, even output dims, source
+// rows of <= WHMAX pixels, and every two consecutive steps' source rows within the ring (checked here
+// over the launch's segments); SFA_E_UNSUPPORTED otherwise.
+template <int K, int OCC>
+inline int launch_fpn_seg_cfg(const ConvArgs& a, hipStream_t st) {
+  using namespace fpn_seg;
+  static_assert(OCC * lds_bytes(K) <= 160 * 1024, "blocks per CU vs LDS");
+  const ConvSeg& g = a.seg[0];
+  if (a.nseg != 1 || g.KH != 1 || g.KW != 1 || g.stride != 1 || g.pad != 0 || g.C != K || a.Kpad != K ||
+      a.N % NB != 0 || !a.wh || !a.winv || a.res || !a.res_up || a.ksplit > 1 || a.OH != g.H || a.OW != g.W ||
+      a.OH % 2 || a.OW % 2 || a.OW / 2 > WHMAX || (a.wstride && (a.wstride < a.wk0 + K || a.wk0 % 8 != 0)))
+    return SFA_E_UNSUPPORTED;
+  const int frames = a.M / (a.OH * a.OW);
+  if (frames <= 0) return SFA_OK;
+  if ((size_t)frames * a.OH * a.OW * K * 4 >= (1ull << 31) ||
+      (size_t)frames * (a.OH / 2) * (a.OW / 2) * a.N * 4 >= (1ull << 31))
+    return SFA_E_UNSUPPORTED;
+  const int ncu = cu_count(st);
+  const int nct = a.N / NB;
+  int segs = (OCC * ncu + frames * nct - 1) / (frames * nct);  // about OCC blocks per CU
+  segs = segs < 1 ? 1 : (segs > a.OH ? a.OH : segs);
+  // the ring holds every two consecutive steps' source rows (the same for every frame)
+  const int H = a.OH, W = a.OW, Hh = H / 2;
+  for (int sk = 0; sk < segs; ++sk) {
+    const int pb = (sk * H / segs) * W, pe = ((sk + 1) * H / segs) * W;
+    for (int p = pb; p < pe; p += P) {
+      int lo, hi, lo2 = 0, hi2 = 0;
+      step_rows(p, pe, W, Hh, a.res_sh, lo, hi);
+      if (p + P < pe) step_rows(p + P, pe, W, Hh, a.res_sh, lo2, hi2);
+      if (max(hi, hi2) - lo + 1 > NSLOT || (p + P < pe && lo2 < lo)) return SFA_E_UNSUPPORTED;
+    }
+  }
+  hipLaunchKernelGGL((fpn_seg_kernel<K, OCC>), dim3((unsigned)(frames * segs * nct)), dim3(NT), 0, st, a, segs);
   SFA_LAUNCH_CHECK();
   return SFA_OK;
 }

@@ -289,10 +289,12 @@ struct sfa_model {
   int stem_patch = 1;
   // fp16x3 FPN 1x1 convs on the persistent kernels of fpn_kernel.h, mask (env SFA_FPN_GEMM): bit f =
   // level f's low-resolution W_a . x conv (weight-resident row streaming), bit 3 + f = its skip conv
-  // with the upsampled residual (level 2: full rows with the taps from an LDS ring); the other convs
-  // run on conv_h3 / conv_r3 (the same products for the skip convs). Default 37 = the low-res convs of
-  // levels 0 and 2 and the level-2 skip conv, the ones measured faster (profiles/r04d_*, r04l_*)
-  int fpn_gemm = 37;
+  // with the upsampled residual (level 2: full rows with the taps from an LDS ring; levels 0 / 1: flat
+  // pixel steps, fpn_seg_kernel); the other convs run on conv_h3 / conv_r3 (the same products for the
+  // skip convs). Default 61 = the low-res convs of levels 0 and 2 and the three skip convs, the ones
+  // measured faster (profiles/r04d_*, r04l_*, r05n_*); 63 (level 1's low-res conv too: -5 us serial, other
+  // bits within 2e-5) measured bench-equal
+  int fpn_gemm = 61;
   // fp16x3 split-K layer4 strip convs: 1 (default) = the last slice of each tile combines the partials in
   // the conv kernel (tickets, conv_h3_kernel.h splitk_ticket), 0 = splitk_reduce_kernel launches; the
   // same bits (env SFA_SPLITK_TICKETS). conv_h3's split convs keep the reduce launch.

@@ -194,7 +194,7 @@ def test_argument_errors_before_any_launch():
         assert L.sfa_model_probe_times(h, ms, 4) == -1
         # kernel-choice options live in the handle (no env reads on the launch path)
         v = ctypes.c_int()
-        defaults = {_lib.OPT_STEM_PATCH: 1, _lib.OPT_FPN_COMMUTE: 7, _lib.OPT_FPN_GEMM: 37,
+        defaults = {_lib.OPT_STEM_PATCH: 1, _lib.OPT_FPN_COMMUTE: 7, _lib.OPT_FPN_GEMM: 61,
                     _lib.OPT_SPLITK_TICKETS: 1}
         assert len(defaults) == _lib.OPT_COUNT
         for key, val in defaults.items():

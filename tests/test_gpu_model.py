@@ -317,6 +317,25 @@ def test_fpn_gemm_kernel_choices(golden, gpu, hw):
                 assert float(np.max(np.abs(res[mask][h] - r) / np.maximum(1.0, np.abs(r)))) <= 1e-4, (h, mask)
 
 
+@pytest.mark.parametrize("bs", [16, 7])
+def test_fpn_seg_kernel_multistep(golden, gpu, bs):
+    """The level-0 / level-1 skip convs on fpn_seg_kernel (flat 128-pixel steps over a frame segment,
+    the residual's source rows in an LDS ring; SFA_OPT_FPN_GEMM bits 3 / 4) at 608 x 608 with batches
+    that give segments of several steps (bs 16: 6 / 3 steps per segment, bs 7: 3 / 2 steps, ragged segment bounds): the same
+    bits as the per-tile conv_r3 skip convs (mask 37 vs 61)."""
+    x = torch.from_numpy(synthetic.synthetic_bev(bs, 608, 608, seed=23)).to(gpu)
+    res = {}
+    for mask in (37, 61):
+        model = make_model(golden, gpu)
+        eng = model._engine(gpu)
+        eng.set_math(_math("fp16x3"))
+        eng.set_option(_lib.OPT_FPN_GEMM, mask)
+        with torch.no_grad():
+            res[mask] = {h: v.cpu().numpy() for h, v in model(x).items()}
+    for h in gc.HEADS:
+        np.testing.assert_array_equal(res[61][h], res[37][h], err_msg=f"{h}: fpn_seg vs conv_r3 skip convs")
+
+
 def test_splitk_tickets_bit_identical(golden, gpu):
     """SFA_OPT_SPLITK_TICKETS: the split-K layer4 strip convs combine their two K-slices in the conv
     kernel (the last slice of each tile to finish, by an agent-scope atomic ticket, reads the other's
@@ -366,7 +385,7 @@ def test_fpn_gemm_batch_over_256_frames(golden, gpu):
     model = make_model(golden, gpu)
     eng = model._engine(gpu)
     eng.set_math(_math("fp16x3"))
-    assert eng.get_option(_lib.OPT_FPN_GEMM) == 37
+    assert eng.get_option(_lib.OPT_FPN_GEMM) == 61
     with torch.no_grad():
         full = {h: v[255:257].cpu().numpy() for h, v in model(x).items()}
         two = {h: v.cpu().numpy() for h, v in model(x[255:257].contiguous()).items()}
