@@ -151,11 +151,34 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
   const int M = a.M, lane = tid & 63, c16 = lane & 15, g = lane >> 4;
   float* WH = reinterpret_cast<float*>(smem);  // [HPB][4][64]: w1 * winv
   float* BP = WH + HPB * 256;                  // [HPB * 64]: bias / winv
-  for (int i = tid; i < HPB * 256; i += NT) {
-    const int n = n0 + (i >> 8) * 64 + (i & 63);
-    WH[i] = a.hw1[nt * HPB * 256 + i] * a.winv[n];
+  // every load in flight before the first product, the heads' output biases too (round 5: the
+  // element-wise loops waited one L2 round trip per iteration, and each head's bias load, ordered
+  // after the previous head's stores, one more: up to nine per tile); indices clamped, no branch
+  float hbv[HPB];
+  {
+    constexpr int NI = (HPB * 256 + NT - 1) / NT, NJ = (HPB * 64 + NT - 1) / NT;
+    float hv[NI], wv[NI], bv[NJ], bw[NJ];
+#pragma unroll
+    for (int hh = 0; hh < HPB; ++hh) hbv[hh] = a.hb1[(nt * HPB + hh) * 4 + (lane >> 4)];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int i = min(tid + j * NT, HPB * 256 - 1);
+      hv[j] = a.hw1[nt * HPB * 256 + i];
+      wv[j] = a.winv[n0 + (i >> 8) * 64 + (i & 63)];
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int i = min(tid + j * NT, HPB * 64 - 1);
+      bv[j] = a.bias[n0 + i];
+      bw[j] = a.winv[n0 + i];
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+      if (tid + j * NT < HPB * 256) WH[tid + j * NT] = hv[j] * wv[j];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+      if (tid + j * NT < HPB * 64) BP[tid + j * NT] = bv[j] / bw[j];
   }
-  for (int i = tid; i < HPB * 64; i += NT) BP[i] = a.bias[n0 + i] / a.winv[n0 + i];
   __syncthreads();
   auto swap_add32 = [](float& x, float& y) {  // x: sum over (l, l^32) in lanes < 32; y: in lanes >= 32
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
@@ -249,7 +272,7 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
     // level 2 (l ^ 16): even rows keep the first of each pair, odd rows the second -> lane g: output g
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) swap_add16(p[mi][0], p[mi][1]);
-    const float hb = a.hb1[head * 4 + g];
+    const float hb = hbv[hh];
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
       const int m = mrow0 + mi * 16 + c16;

@@ -185,6 +185,36 @@ __global__ void __launch_bounds__(256) stem_pool_merge_kernel(const ConvArgs a, 
   *reinterpret_cast<x6_f32x4*>(dst) = m;
 }
 
+// The stem's split weights wh [2][64][Kpad] (k = (kh 7 + kw) 4 + c) -> LDS [2][64][WROW] at
+// k' = (kh 8 + kw) 4 + c, the kw = 7 column zero: every load in flight before the first store (round 5:
+// the load -> store loop waited one memory latency per iteration, 14 per block).
+template <int NT, int WROW>
+__device__ __forceinline__ void stem_stage_w(const ConvArgs& a, unsigned char* SW, int tid) {
+  constexpr int ITEMS = 2 * 64 * 56, NWI = (ITEMS + NT - 1) / NT;
+  // branch-free buffer loads: the kw = 7 column and the tail read out of range (zeros)
+  const __amdgpu_buffer_rsrc_t rsw = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(a.wh), (short)0,
+                                                                       2 * 64 * a.Kpad * 2, 0x00020000);
+  using u32x2 = unsigned __attribute__((ext_vector_type(2)));
+  u32x2 wv[NWI];
+#pragma unroll
+  for (int j = 0; j < NWI; ++j) {
+    const int i = tid + j * NT;
+    const int t = i / (64 * 56), rem = i - t * (64 * 56);
+    const int n = rem / 56, tap = rem - n * 56;
+    const int kh = tap >> 3, kw = tap & 7;
+    const unsigned off =
+        i < ITEMS && kw < 7 ? (unsigned)(((t * 64 + n) * a.Kpad + (kh * 7 + kw) * 4) * 2) : 0x80000000u;
+    wv[j] = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rsw, off, 0, 0));
+  }
+#pragma unroll
+  for (int j = 0; j < NWI; ++j) {
+    const int i = tid + j * NT;
+    const int t = i / (64 * 56), rem = i - t * (64 * 56);
+    const int n = rem / 56, tap = rem - n * 56;
+    if (i < ITEMS) *reinterpret_cast<u32x2*>(SW + t * 64 * WROW + n * WROW + tap * 8) = wv[j];
+  }
+}
+
 // ABL (timing ablations only, env SFA_STEM_ABL; results wrong): 1 = no epilogue, 2 = no MFMAs,
 // 4 = no patch fetch, 8 = first patch fetched after the weights are staged,
 // 16 = border cells stored instead of atomicMax (only with a.part == null: the atomic A/B form),
@@ -275,16 +305,7 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool_kernel(const ConvArgs 
     if (tile + G < ntiles) fetch(tile + G, pf1);
   }
   // weights: wh [2][64][Kpad] with k = (kh 7 + kw) 4 + c  ->  LDS [2][64][WROW] at k' = (kh 8 + kw) 4 + c
-#pragma unroll
-  for (int i = tid; i < 2 * 64 * 56; i += NT) {
-    const int t = i / (64 * 56), rem = i - t * (64 * 56);
-    const int n = rem / 56, tap = rem - n * 56;
-    const int kh = tap >> 3, kw = tap & 7;
-    uint2 v = make_uint2(0u, 0u);
-    if (kw < 7)
-      v = *reinterpret_cast<const uint2*>(a.wh + ((size_t)t * 64 + n) * a.Kpad + (kh * 7 + kw) * 4);
-    *reinterpret_cast<uint2*>(SW + t * 64 * WROW + n * WROW + tap * 8) = v;
-  }
+  stem_stage_w<NT, WROW>(a, SW, tid);
 
   if (!(ABL & 4) && (ABL & 8)) {
     if (tile < ntiles) fetch(tile, pf0);
@@ -528,14 +549,7 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool2_kernel(const ConvArgs
   if (t0 < ntiles) fetch(t0, R0);
   if (t0 + G < ntiles) fetch(t0 + G, R1);
   // weights: wh [2][64][Kpad], k = (kh 7 + kw) 4 + c  ->  LDS [2][64][WROW] at k' = (kh 8 + kw) 4 + c
-  for (int i = tid; i < 2 * 64 * 56; i += NT) {
-    const int t = i / (64 * 56), rem = i - t * (64 * 56);
-    const int n = rem / 56, tap = rem - n * 56;
-    const int kh = tap >> 3, kw = tap & 7;
-    uint2 v = make_uint2(0u, 0u);
-    if (kw < 7) v = *reinterpret_cast<const uint2*>(a.wh + ((size_t)t * 64 + n) * a.Kpad + (kh * 7 + kw) * 4);
-    *reinterpret_cast<uint2*>(SW + t * 64 * WROW + n * WROW + tap * 8) = v;
-  }
+  stem_stage_w<NT, WROW>(a, SW, tid);
   if (t0 >= ntiles) return;  // uniform per block
   patch_max(R0, WMX);
   __syncthreads();
