@@ -145,23 +145,20 @@ __device__ __forceinline__ void r3t_epilogue_std(const ConvArgs& a, f32x4_t (&ac
 // of each of its pixels (3 swaps + 3 adds per sub-tile, all VALU, no LDS, no barrier per head). The per-channel
 // weight scale winv = 2^-e (fp16x3) is folded into the staged 1x1 weights and biases
 // (w1 * winv, b / winv: exact power-of-two scalings), so T = max(acc * ainv + b', 0).
-template <int TM, int TN, int NT, int HPB, bool PK = false>
-__device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* smem,
-                                                  int mrow0, int n0, int nt, int tid, const float (&ainv)[TM]) {
-  const int M = a.M, lane = tid & 63, c16 = lane & 15, g = lane >> 4;
-  float* WH = reinterpret_cast<float*>(smem);  // [HPB][4][64]: w1 * winv
-  float* BP = WH + HPB * 256;                  // [HPB * 64]: bias / winv
-  // every load in flight before the first product, the heads' output biases too (round 5: the
-  // element-wise loops waited one L2 round trip per iteration, and each head's bias load, ordered
-  // after the previous head's stores, one more: up to nine per tile); indices clamped, no branch
-  float hbv[HPB];
-  {
-    constexpr int NI = (HPB * 256 + NT - 1) / NT, NJ = (HPB * 64 + NT - 1) / NT;
-    float hv[NI], wv[NI], bv[NJ], bw[NJ];
+// The heads epilogue's constants for column tile nt (w1 * winv, bias / winv, the 1x1 biases) into LDS at
+// HS: loads first, then the stores (the caller's barrier publishes them).  Round 5: staged once per
+// block in the prologue, where the loads overlap the first W DMA, instead of after the K loop, where
+// their L2 round trips (up to nine per tile before round 5) and a barrier sat between the last MFMAs
+// and the first head products.
+template <int NT, int HPB>
+struct R3HeadStage {
+  static constexpr int NI = (HPB * 256 + NT - 1) / NT, NJ = (HPB * 64 + NT - 1) / NT;
+  static constexpr int BYTES = HPB * (256 + 64 + 4) * 4;
+  float hv[NI], wv[NI], bv[NJ], bw[NJ], hb;
+  __device__ __forceinline__ void load(const ConvArgs& a, int n0, int nt, int tid) {
+    hb = a.hb1[nt * HPB * 4 + min(tid, HPB * 4 - 1)];
 #pragma unroll
-    for (int hh = 0; hh < HPB; ++hh) hbv[hh] = a.hb1[(nt * HPB + hh) * 4 + (lane >> 4)];
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
+    for (int j = 0; j < NI; ++j) {  // indices clamped: no branch around the loads
       const int i = min(tid + j * NT, HPB * 256 - 1);
       hv[j] = a.hw1[nt * HPB * 256 + i];
       wv[j] = a.winv[n0 + (i >> 8) * 64 + (i & 63)];
@@ -172,14 +169,26 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
       bv[j] = a.bias[n0 + i];
       bw[j] = a.winv[n0 + i];
     }
+  }
+  __device__ __forceinline__ void store(float* HS, int tid) const {
 #pragma unroll
     for (int j = 0; j < NI; ++j)
-      if (tid + j * NT < HPB * 256) WH[tid + j * NT] = hv[j] * wv[j];
+      if (tid + j * NT < HPB * 256) HS[tid + j * NT] = hv[j] * wv[j];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
-      if (tid + j * NT < HPB * 64) BP[tid + j * NT] = bv[j] / bw[j];
+      if (tid + j * NT < HPB * 64) HS[HPB * 256 + tid + j * NT] = bv[j] / bw[j];
+    if (tid < HPB * 4) HS[HPB * 320 + tid] = hb;
   }
-  __syncthreads();
+};
+
+template <int TM, int TN, int NT, int HPB, bool PK = false>
+__device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&acc)[TM][TN], const unsigned char* smem,
+                                                  int mrow0, int n0, int nt, int tid, const float (&ainv)[TM]) {
+  const int M = a.M, lane = tid & 63, c16 = lane & 15, g = lane >> 4;
+  // staged once per block in the prologue (r3_stage_head, its own LDS region: round 5)
+  const float* WH = reinterpret_cast<const float*>(smem);  // [HPB][4][64]: w1 * winv
+  const float* BP = WH + HPB * 256;                        // [HPB * 64]: bias / winv
+  const float* HB = BP + HPB * 64;                         // [HPB][4]: the 1x1 convs' biases
   auto swap_add32 = [](float& x, float& y) {  // x: sum over (l, l^32) in lanes < 32; y: in lanes >= 32
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(y), false, false);
     x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
@@ -272,7 +281,7 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
     // level 2 (l ^ 16): even rows keep the first of each pair, odd rows the second -> lane g: output g
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) swap_add16(p[mi][0], p[mi][1]);
-    const float hb = hbv[hh];
+    const float hb = HB[hh * 4 + g];
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
       const int m = mrow0 + mi * 16 + c16;
@@ -336,7 +345,9 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   constexpr int NB_REM = ND_B % NW;  // if != 0: waves < NB_REM issue NB pieces, the rest NB - 1
   static_assert(BM % WM == 0 && WM % 16 == 0 && BN % 16 == 0 && TERM_B % 1024 == 0, "tile");
   static_assert(TN >= 2, "two W blocks in flight");
-  constexpr int EPI_BYTES = EPI == EPI_HEAD ? BM * 65 * 4 + (BN / 64) * 1024 : 2 * NW * 4;
+  // heads: the epilogue's constants in their own region after the W stages (R3HeadStage)
+  constexpr int HS_OFF = NSTAGE * STAGE;
+  constexpr int EPI_BYTES = EPI == EPI_HEAD ? HS_OFF + R3HeadStage<NT, BN / 64>::BYTES : 2 * NW * 4;
   constexpr int LDS_BYTES = NSTAGE * STAGE > EPI_BYTES ? NSTAGE * STAGE : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
 
@@ -353,6 +364,9 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   const int mt = lbid / n_tiles, nt = lbid - mt * n_tiles;
   const int m0 = mt * BM, n0 = nt * BN;
   const int M = a.M;
+  // heads: the epilogue's constants in flight during the whole prologue (stored before its barrier)
+  [[maybe_unused]] R3HeadStage<NT, BN / 64> hst;
+  if constexpr (EPI == EPI_HEAD) hst.load(a, n0, nt, tid);
 
   // ---- A: this lane's rows (one per 16-row sub-tile), gather origins per segment ----
   // (round 5: row decomposition by multiply-high divisions, a.fd_ow / a.fd_oh from the launch)
@@ -545,8 +559,11 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   constexpr int NA_OPS = 2 * TM;  // A loads per K-tile (issued after the tile's W DMA)
   // prologue: W tile 0 (the stagger's first interval DMAs tile 1), A tile 0; this wave's W
   // landed, then everyone's
+  // (heads: the epilogue's constants, loaded at the top of the body, stored here once they land and
+  // published by this barrier)
   if (nk > 0) load_w(kt0, smem);
   load_a(kt0);
+  if constexpr (EPI == EPI_HEAD) hst.store(reinterpret_cast<float*>(smem + HS_OFF), tid);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA_OPS) : "memory");
   __builtin_amdgcn_s_barrier();
   if constexpr ((ABL & 4) != 0) {
@@ -684,11 +701,13 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
       }
     return;
   }
-  __syncthreads();
-  if constexpr (EPI == EPI_HEAD)
-    r3t_epilogue_head<TM, TN, NT, BN / 64, (ABL & 65536) != 0>(a, acc, smem, m0 + wave * WM, n0, nt, tid, ainv);
-  else
+  if constexpr (EPI == EPI_HEAD) {  // reads only the constants' region: no barrier after the K loop
+    r3t_epilogue_head<TM, TN, NT, BN / 64, (ABL & 65536) != 0>(a, acc, smem + HS_OFF, m0 + wave * WM, n0, nt, tid,
+                                                              ainv);
+  } else {
+    __syncthreads();
     r3t_epilogue_std<TM, TN, NT, (ABL & 32768) != 0, false>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv);
+  }
 }
 
 template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int NSEG, int ABL = 0>

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise tools/headstampbench output (s_memtime stamps of the fused heads kernel, round 5): per
-wave the prologue (start -> after the first barrier), the K loop and the epilogue; the K-tile barrier
-waits; and per CU the idle gap between one tile's last wave ending and the next tile's first wave
+wave the prologue (start -> after the first barrier), the K loop and the epilogue; the K-tile memory waits (vmcnt) and
+barriers by wave half; and per CU the idle gap between one tile's last wave ending and the next tile's first wave
 starting (block turnover), as shares of the CU's busy time.
 
   python tools/head_stamp_summary.py gpurun_out/hstamps_L1.bin
@@ -29,12 +29,16 @@ def main(path):
     st("epilogue", epi)
     st("tile lifetime (wave)", life)
     k = min(nkt, NKT_MAX)
-    bw = d[:, :, 6:6 + 2 * k:2] - d[:, :, 5:5 + 2 * k:2]
-    bw = bw[ok]
-    st("K-tile barrier wait", bw.reshape(-1))
+    vw = (d[:, :, 6:6 + 3 * k:3] - d[:, :, 5:5 + 3 * k:3])
+    bw = (d[:, :, 7:7 + 3 * k:3] - d[:, :, 6:6 + 3 * k:3])
+    for half, sel in (("leading half", slice(0, nw // 2)), ("delayed half", slice(nw // 2, nw))):
+        okh = ok[:, sel]
+        st(f"memory wait, {half}", vw[:, sel][okh].reshape(-1))
+        st(f"barrier, {half}", bw[:, sel][okh].reshape(-1))
+    vws, bws = vw[ok].sum() * nkt / k, bw[ok].sum() * nkt / k
     print(f"  shares of the waves' lifetimes: prologue {100 * pro.sum() / life.sum():.1f} %, K loop "
-          f"{100 * loop.sum() / life.sum():.1f} % (barrier waits ~{100 * bw.sum() * nkt / k / life.sum():.1f} %), "
-          f"epilogue {100 * epi.sum() / life.sum():.1f} %")
+          f"{100 * loop.sum() / life.sum():.1f} % (memory waits ~{100 * vws / life.sum():.1f} %, barriers "
+          f"~{100 * bws / life.sum():.1f} %), epilogue {100 * epi.sum() / life.sum():.1f} %")
     # per CU: tiles in start order, the gap from a tile's end (last wave) to the next tile's start (first wave)
     hw = d[:, 0, 4]
     cu = ((hw >> 32) << 16) | ((hw & 0xffffffff) >> 8 & 0xff)
