@@ -145,7 +145,7 @@ static const size_t g_part_floats = 64u << 20;
   }
 #define CANDH3(BM, BN, WM, OCC, NK, NST, KS)                                                        \
   Cand {                                                                                          \
-    "h3 " #BM "x" #BN " w" #WM " occ" #OCC " ks" #KS, 32, [](const ConvArgs& a, hipStream_t s) {   \
+    "h3 " #BM "x" #BN " w" #WM " occ" #OCC " st" #NST " ks" #KS, 32, [](const ConvArgs& a, hipStream_t s) {   \
       ConvArgs b = a;                                                                             \
       b.ksplit = KS;                                                                              \
       b.part = g_part;                                                                            \
@@ -242,6 +242,8 @@ int main(int argc, char** argv) {
       CANDR(128, 128, 32, EPI_STD, 2, 2, 526592, 1), CANDH3(128, 128, 32, 2, 32, 2, 1),
       CANDR(64, 128, 16, EPI_STD, 3, 2, 526592, 1), CANDR(64, 128, 32, EPI_STD, 4, 2, 526592, 1),
       CANDR(128, 128, 32, EPI_STD, 2, 2, 526592, 1), CANDH3(128, 128, 32, 2, 32, 2, 1),
+      // round 5: deeper W / A rings for conv_h3 (one block per CU)
+      CANDH3(128, 128, 32, 1, 32, 3, 1), CANDH3(128, 128, 32, 1, 32, 4, 1), CANDH3(128, 128, 32, 2, 32, 2, 1),
   };
   // layer4.0.conv1 (M 5776, N 512): the product's conv_h3 128 x 128 with split-K 2 against other
   // splits and the 64-row conv_r3 tiles with split-K
@@ -250,6 +252,7 @@ int main(int argc, char** argv) {
       CANDR(128, 128, 32, EPI_STD, 2, 2, 526592, 2), CANDH3(128, 128, 32, 2, 32, 2, 3),
       CANDH3(128, 128, 32, 2, 32, 2, 4), CANDR(64, 128, 16, EPI_STD, 3, 2, 526592, 3),
       CANDR(64, 128, 16, EPI_STD, 3, 2, 526592, 4), CANDH3(128, 128, 32, 2, 32, 2, 2),
+      CANDH3(128, 128, 32, 1, 32, 3, 2), CANDH3(128, 128, 32, 1, 32, 4, 2), CANDH3(128, 128, 32, 2, 32, 2, 2),
   };
   std::vector<Cand> heads = {
       CANDR(256, 320, 32, EPI_HEAD, 1, 3, 1669380, 1),
