@@ -436,7 +436,9 @@ namespace stem_patch2 {
 using namespace stem_patch;
 constexpr int XCH_W = 9 * 64 * 4;                  // one wave's second-row horizontal maxima
 constexpr int XCH_BYTES = NW * XCH_W;              // per buffer
-constexpr int LDS2 = W_BYTES + 2 * 2 * PATCH_TERM + 2 * XCH_BYTES + 2 * 2 * NW * 4;  // 141,376 B
+// + the output channels' winv / bias (round 5: read from LDS in the epilogue instead of 8 global loads
+// per tile, which hipcc issued as four dependent round trips)
+constexpr int LDS2 = W_BYTES + 2 * 2 * PATCH_TERM + 2 * XCH_BYTES + 2 * 2 * NW * 4 + 2 * 64 * 4;  // 141,888 B
 }  // namespace stem_patch2
 
 template <int IN = STEM_IN_NHWC4, int ABL = 0>
@@ -449,6 +451,7 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool2_kernel(const ConvArgs
   float* XCH0 = reinterpret_cast<float*>(SU0 + 4 * PATCH_TERM);      // [2][NW][9][64]
   float* WMX = XCH0 + 2 * XCH_BYTES / 4;                             // [2][NW] patch maxima
   float* TMX = WMX + 2 * NW;                                         // [2][NW] tile (ReLU) maxima
+  float* CSB = TMX + 2 * NW;                                         // [64] winv, [64] bias
   const ConvSeg& g = a.seg[0];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -550,6 +553,11 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool2_kernel(const ConvArgs
   if (t0 + G < ntiles) fetch(t0 + G, R1);
   // weights: wh [2][64][Kpad], k = (kh 7 + kw) 4 + c  ->  LDS [2][64][WROW] at k' = (kh 8 + kw) 4 + c
   stem_stage_w<NT, WROW>(a, SW, tid);
+  if (tid < 64) {  // published by the first tile's barriers
+    const float wv = a.winv[tid], bv = a.bias[tid];
+    CSB[tid] = wv;
+    CSB[64 + tid] = bv;
+  }
   if (t0 >= ntiles) return;  // uniform per block
   patch_max(R0, WMX);
   __syncthreads();
@@ -662,8 +670,8 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool2_kernel(const ConvArgs
 #pragma unroll
     for (int ni = 0; ni < 4; ++ni) {
       const int n = ni * 16 + c16;
-      const float bn = a.bias[n];
-      const float cs = a.winv[n] * ainv_cur;
+      const float bn = CSB[64 + n];
+      const float cs = CSB[n] * ainv_cur;
 #pragma unroll
       for (int mi = 0; mi < 2; ++mi) {
         float v[4];
