@@ -467,6 +467,11 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool2_kernel(const ConvArgs
   constexpr int NG = (PW + 1 + 3) / 4;  // column groups per patch row: 10
   static_assert(!VEC || PH * NG <= NT, "one item per thread");
   x6_f32x4 R0[PF], R1[PF];
+  // branch-free buffer loads (out-of-range offsets read zeros): no zeroing of the patch registers
+  // ahead of a conditional load, which made hipcc wait for every outstanding store first (round 5)
+  const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(g.x), (short)0,
+      (int)((size_t)(ntiles / tiles_per_frame) * (VEC ? 3 : 4) * g.H * g.W * 4), 0x00020000);
   auto fetch = [&](int tile, x6_f32x4 (&pf)[PF]) {
     const int b = tile / tiles_per_frame, tl = tile - b * tiles_per_frame;
     const int th = tl / tw_n, tw = tl - th * tw_n;
@@ -475,19 +480,15 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool2_kernel(const ConvArgs
     if constexpr (VEC) {
       const int py = tid / NG, q = tid - py * NG;
       const int iy = iy0 + py, ixg = ix0 - 1 + 4 * q;
-      x6_f32x4 z = {0.f, 0.f, 0.f, 0.f};
-      pf[0] = z;
-      pf[1] = z;
-      pf[2] = z;
-      if (py < PH && (unsigned)iy < (unsigned)g.H && (unsigned)ixg < (unsigned)g.W) {
-        const int sy = IN == STEM_IN_NCHW3_FLIP ? g.H - 1 - iy : iy;
-        const int sx = IN == STEM_IN_NCHW3_FLIP ? g.W - 4 - ixg : ixg;
-        const float* x = g.x + (size_t)b * 3 * hw + (size_t)sy * g.W + sx;
+      const bool ok = py < PH && (unsigned)iy < (unsigned)g.H && (unsigned)ixg < (unsigned)g.W;
+      const int sy = IN == STEM_IN_NCHW3_FLIP ? g.H - 1 - iy : iy;
+      const int sx = IN == STEM_IN_NCHW3_FLIP ? g.W - 4 - ixg : ixg;
+      const unsigned base = (unsigned)(((size_t)b * 3 * hw + (size_t)sy * g.W + sx) * 4);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          const x6_f32x4 v = *reinterpret_cast<const x6_f32x4*>(x + c * hw);
-          pf[c] = IN == STEM_IN_NCHW3_FLIP ? x6_f32x4{v[3], v[2], v[1], v[0]} : v;
-        }
+      for (int c = 0; c < 3; ++c) {
+        const x6_f32x4 v = __builtin_bit_cast(
+            x6_f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsx, ok ? base + (unsigned)(c * hw * 4) : 0x80000000u, 0, 0));
+        pf[c] = IN == STEM_IN_NCHW3_FLIP ? x6_f32x4{v[3], v[2], v[1], v[0]} : v;
       }
     } else {
 #pragma unroll
@@ -495,10 +496,9 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool2_kernel(const ConvArgs
         const int p = tid + j * NT;
         const int py = p / PW, px = p - py * PW;
         const int iy = iy0 + py, ix = ix0 + px;
-        x6_f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (p < PIX && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W)
-          v = reinterpret_cast<const x6_f32x4*>(g.x)[(size_t)b * hw + iy * g.W + ix];
-        pf[j] = v;
+        const bool ok = p < PIX && (unsigned)iy < (unsigned)g.H && (unsigned)ix < (unsigned)g.W;
+        pf[j] = __builtin_bit_cast(x6_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                 rsx, ok ? (unsigned)(((size_t)b * hw + iy * g.W + ix) * 16) : 0x80000000u, 0, 0));
       }
     }
   };
@@ -742,12 +742,29 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
     return SFA_E_INVALID;
   }
   if (al16 || a.stem_in == STEM_IN_NHWC4) {
-    switch (a.stem_in) {
-      case STEM_IN_NCHW3: hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3, 1>), gd, bd, 0, st, a, ntiles); break;
-      case STEM_IN_NCHW3_FLIP:
-        hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3_FLIP, 1>), gd, bd, 0, st, a, ntiles);
-        break;
-      default: hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NHWC4, 1>), gd, bd, 0, st, a, ntiles); break;
+    // the kernel reads the input through a buffer resource with 32-bit offsets: batches whose input
+    // reaches 2 GiB run in frame chunks (the side-buffer slots keep their global tile index)
+    const size_t fbytes = (size_t)(a.stem_in == STEM_IN_NHWC4 ? 4 : 3) * g.H * g.W * 4;
+    const int fchunk = (int)std::min<size_t>((size_t)frames, ((1ull << 31) - 1) / fbytes);
+    const int tpf = (a.OH / 16) * (a.OW / 16);
+    for (int f0 = 0; f0 < frames; f0 += fchunk) {
+      const int nf = std::min(fchunk, frames - f0);
+      ConvArgs c = a;
+      c.seg[0].x = g.x + (size_t)f0 * (fbytes / 4);
+      c.seg[0].bytes = (size_t)nf * fbytes;
+      c.y = a.y + (size_t)f0 * (a.OH / 2) * (a.OW / 2) * 64;
+      c.part = a.part + (size_t)f0 * tpf * 17 * 64;
+      if (a.amax_out) c.amax_out = a.amax_out + (size_t)f0 * SFA_AMAX_WORDS;
+      c.M = nf * a.OH * a.OW;
+      const int nt = nf * tpf;
+      const dim3 gc((unsigned)(nt < ncu ? nt : ncu));
+      switch (a.stem_in) {
+        case STEM_IN_NCHW3: hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3, 1>), gc, bd, 0, st, c, nt); break;
+        case STEM_IN_NCHW3_FLIP:
+          hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NCHW3_FLIP, 1>), gc, bd, 0, st, c, nt);
+          break;
+        default: hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NHWC4, 1>), gc, bd, 0, st, c, nt); break;
+      }
     }
   } else if (a.stem_in == STEM_IN_NCHW3) {
     hipLaunchKernelGGL((stem_patch_pool_kernel<0, STEM_IN_NCHW3>), gd, bd, 0, st, a, ntiles);

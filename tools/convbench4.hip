@@ -244,6 +244,9 @@ int main(int argc, char** argv) {
       CANDR(128, 128, 32, EPI_STD, 2, 2, 526592, 1), CANDH3(128, 128, 32, 2, 32, 2, 1),
       // round 5: deeper W / A rings for conv_h3 (one block per CU)
       CANDH3(128, 128, 32, 1, 32, 3, 1), CANDH3(128, 128, 32, 1, 32, 4, 1), CANDH3(128, 128, 32, 2, 32, 2, 1),
+      // round 5: split-K 2 / 3 for the stride-2 convs (362 / 722 tiles for 512 / 768 slots without)
+      CANDH3(128, 128, 32, 2, 32, 2, 2), CANDH3(128, 128, 32, 2, 32, 2, 3),
+      CANDR(64, 128, 16, EPI_STD, 3, 2, 526592, 2), CANDR(128, 128, 32, EPI_STD, 2, 2, 526592, 2),
   };
   // layer4.0.conv1 (M 5776, N 512): the product's conv_h3 128 x 128 with split-K 2 against other
   // splits and the 64-row conv_r3 tiles with split-K
