@@ -68,11 +68,20 @@ __device__ __forceinline__ void h3_epilogue16(const ConvArgs& a, f32x4_t (&acc)[
             rv[mi][ni][v] = res_up_sample(a, m, n0 + wn * WN + ni * 16 + c16);
           }
     }
+    // the columns' bias / winv all loaded before the first store (round 5: per column block they sat
+    // behind the previous block's stores, which may alias them for hipcc: one round trip each)
+    float bng[TN], csg[TN];
 #pragma unroll
     for (int ni = 0; ni < TN; ++ni) {
       const int n = n0 + wn * WN + ni * 16 + c16;
-      const float bn = a.bias ? a.bias[n] : 0.f;
-      const float cs = a.winv[n];
+      bng[ni] = a.bias ? a.bias[n] : 0.f;
+      csg[ni] = a.winv[n];
+    }
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) {
+      const int n = n0 + wn * WN + ni * 16 + c16;
+      const float bn = bng[ni];
+      const float cs = csg[ni];
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
 #pragma unroll
@@ -645,6 +654,10 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_h3_kerne
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (nsplit > 1) {  // split-K: this slice's partial sums, scaled back (the reduce adds the rest)
     float* part = a.part + (size_t)kz * M * a.N;
+    // the columns' winv loaded before the first partial store (they may alias for hipcc: round 5)
+    float wvg[TN];
+#pragma unroll
+    for (int ni = 0; ni < TN; ++ni) wvg[ni] = a.winv[n0 + wn * WN + ni * (MF ? 16 : 32) + (MF ? (lane & 15) : (lane & 31))];
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi)
 #pragma unroll
@@ -661,7 +674,7 @@ __global__ void __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) conv_h3_kerne
           }
           const float si = __shfl(ainv[mi], MF ? (row & 15) : (row & 31), 64);
           const int m = m0 + wm * WM + row, n = n0 + wn * WN + col;
-          if (m < M) part[(size_t)m * a.N + n] = acc[mi][ni][v] * si * a.winv[n];
+          if (m < M) part[(size_t)m * a.N + n] = acc[mi][ni][v] * si * wvg[ni];
         }
     return;
   }

@@ -385,7 +385,8 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
         const int m = m0 + wave * WM + mi * 16 + c16, n = n0 + ni * 16 + 4 * gq;
-        const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(a.winv + n);
+        // winv from the LDS copy (a global load here sat behind the previous partial's store)
+        const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(CSB + ni * 16 + 4 * gq);
 #pragma unroll
         for (int v = 0; v < 4; ++v) val[mi][ni][v] = acc[mi][ni][v] * ainv[mi] * cs[v];
         if (m < M) {
@@ -398,28 +399,42 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
       return;
     // the last slice: splitk_reduce_kernel's epilogue on this tile (slice order, + bias, + residual, ReLU)
     AmaxRows am(a.OH * a.OW, m0);
+    // per 16-row sub-tile: the row's slice partials and residual loaded for every column block
+    // first, then summed in slice order and stored (round 5: loaded per block they sat behind the
+    // previous block's store, one round trip each); bias from the LDS copy
 #pragma unroll
-    for (int mi = 0; mi < TM; ++mi)
+    for (int mi = 0; mi < TM; ++mi) {
+      const int m = m0 + wave * WM + mi * 16 + c16;
+      const bool mok = m < M;
+      const int mm = mok ? m : M - 1;
+      x6_f32x4 sv[TN], rr[TN];
 #pragma unroll
       for (int ni = 0; ni < TN; ++ni) {
-        const int m = m0 + wave * WM + mi * 16 + c16, n = n0 + ni * 16 + 4 * gq;
-        if (m >= M) continue;
+        const int n = n0 + ni * 16 + 4 * gq;
         auto part_z = [&](int z) {
           return z == kz ? val[mi][ni]
                          : __builtin_bit_cast(x6_f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                            rsp, (unsigned)((((size_t)z * M + m) * a.N + n) * 4), 0, 16));
+                                                            rsp, (unsigned)((((size_t)z * M + mm) * a.N + n) * 4), 0, 16));
         };
-        x6_f32x4 sv = part_z(0);
-        for (int z = 1; z < nsplit; ++z) sv += part_z(z);
-        sv += *reinterpret_cast<const x6_f32x4*>(a.bias + n);
-        if (a.res) sv += *reinterpret_cast<const x6_f32x4*>(a.res + (size_t)m * a.N + n);
+        sv[ni] = part_z(0);
+        for (int z = 1; z < nsplit; ++z) sv[ni] += part_z(z);
+        rr[ni] = a.res ? *reinterpret_cast<const x6_f32x4*>(a.res + (size_t)mm * a.N + n) : x6_f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int ni = 0; ni < TN; ++ni) {
+        const int n = n0 + ni * 16 + 4 * gq;
+        x6_f32x4 t = sv[ni] + *reinterpret_cast<const x6_f32x4*>(CSB + BN + ni * 16 + 4 * gq);
+        if (a.res) t += rr[ni];
         if (a.relu) {
 #pragma unroll
-          for (int v = 0; v < 4; ++v) sv[v] = fmaxf(sv[v], 0.f);
+          for (int v = 0; v < 4; ++v) t[v] = fmaxf(t[v], 0.f);
         }
-        *reinterpret_cast<x6_f32x4*>(a.y + (size_t)m * a.N + n) = sv;
-        if (a.amax_out) am.add(a.amax_out, m, fmaxf(fmaxf(fabsf(sv[0]), fabsf(sv[1])), fmaxf(fabsf(sv[2]), fabsf(sv[3]))));
+        if (mok) {
+          *reinterpret_cast<x6_f32x4*>(a.y + (size_t)m * a.N + n) = t;
+          if (a.amax_out) am.add(a.amax_out, m, fmaxf(fmaxf(fabsf(t[0]), fabsf(t[1])), fmaxf(fabsf(t[2]), fabsf(t[3]))));
+        }
       }
+    }
     if (a.amax_out) amax_commit_block<NT / 64>(a.amax_out, am.fb0, am.mx0, am.mx1, reinterpret_cast<float*>(smem));
     return;
   }

@@ -39,16 +39,18 @@ struct FpnGeom {
   static constexpr int KC = KT < KCM ? KT : KCM;   // K-tiles per A chunk
   static constexpr int NCH = KT / KC;              // chunks per row tile
   static constexpr int BROW = 64, TERM_B = BN * BROW, STAGE = 2 * TERM_B, W_BYTES = KT * STAGE;
-  static constexpr int LDS = W_BYTES + kFpnMaxFrames * 4 + 2 * 2 * NW * 4;  // 2 amax reduction buffers
+  static constexpr int LDS = W_BYTES + kFpnMaxFrames * 4 + 2 * 2 * NW * 4 + 2 * BN * 4;  // 2 amax buffers, winv / bias
   static_assert(K % 32 == 0 && KT % KC == 0 && BN % 16 == 0 && BN >= 16, "fpn geometry");
 };
 
 // r3t_epilogue_std's arithmetic (same rounding sequence: fmaf(acc * ainv, winv, b), + the
 // bilinear tap value, ReLU) one 16-column block at a time, the block's residual taps loaded just
 // before use (sched_barrier between blocks: hoisting every block's taps spilled at <= 128 VGPRs).
+// csl: the block's columns' winv [TN * 16] and bias [TN * 16] in LDS (staged once per block: round 5,
+// a global load per column block sat behind the previous block's stores)
 template <int TM, int TN, int NT, bool RU>
 __device__ __forceinline__ void fpn_epilogue(const ConvArgs& a, f32x4_t (&acc)[TM][TN], unsigned char* red, int mrow0,
-                                             int m0, int n0, int lane, const float (&ainv)[TM]) {
+                                             int m0, int n0, int lane, const float (&ainv)[TM], const float* csl) {
 #pragma clang fp contract(off)
   const int M = a.M, c16 = lane & 15, g = lane >> 4;
   AmaxRows am(a.OH * a.OW, m0);
@@ -79,8 +81,8 @@ __device__ __forceinline__ void fpn_epilogue(const ConvArgs& a, f32x4_t (&acc)[T
 #pragma unroll
   for (int ni = 0; ni < TN; ++ni) {
     const int n = n0 + ni * 16 + 4 * g;
-    const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(a.winv + n);
-    const x6_f32x4 bn = a.bias ? *reinterpret_cast<const x6_f32x4*>(a.bias + n) : x6_f32x4{0.f, 0.f, 0.f, 0.f};
+    const x6_f32x4 cs = *reinterpret_cast<const x6_f32x4*>(csl + ni * 16 + 4 * g);
+    const x6_f32x4 bn = *reinterpret_cast<const x6_f32x4*>(csl + TN * 16 + ni * 16 + 4 * g);
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
       const int m = mrow0 + mi * 16 + c16;
@@ -154,6 +156,7 @@ __global__ void __launch_bounds__(256, OCC) fpn_gemm_kernel(const ConvArgs a, in
   // the commit's barrier, and a wave that runs ahead into tile t + 1 writes the other buffer (tile
   // t + 2 comes after tile t + 1's barrier, which thread 0 only reaches once it has read them)
   unsigned char* const RED = smem + G::W_BYTES + kFpnMaxFrames * 4;
+  float* const CSL = reinterpret_cast<float*>(RED + 2 * 2 * NW * 4);  // [BN] winv, [BN] bias
   auto swzB = [](int R) { return ((R >> 2) & 3) ^ ((((R & 15) + 4) >> 3) & 1); };
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -164,6 +167,8 @@ __global__ void __launch_bounds__(256, OCC) fpn_gemm_kernel(const ConvArgs a, in
 
   // the weight slice (columns n0 .. n0 + BN - 1, K columns from wk0) and the frame scales -> LDS
   fpn_stage_w<G::KT, BN, NW>(a, n0, smem, wave, lane);
+  static_assert(2 * BN <= NT, "one winv / bias entry per thread");
+  if (tid < 2 * BN) CSL[tid] = tid < BN ? a.winv[n0 + tid] : (a.bias ? a.bias[n0 + tid - BN] : 0.f);
   for (int f = tid; f < nframes; f += NT) {
     float sinv;
     FS[f] = amax_frame_scale(a.amax_in, 1, f, sinv);
@@ -230,7 +235,7 @@ __global__ void __launch_bounds__(256, OCC) fpn_gemm_kernel(const ConvArgs a, in
         }
       }
     }
-    if (c == NCH - 1) fpn_epilogue<TM, TN, NT, RU>(a, acc, RED + (t & 1) * 2 * NW * 4, m0 + wave * WM, m0, n0, lane, ainv);
+    if (c == NCH - 1) fpn_epilogue<TM, TN, NT, RU>(a, acc, RED + (t & 1) * 2 * NW * 4, m0 + wave * WM, m0, n0, lane, ainv, CSL);
   };
   // two chunks in flight: the next one's loads issued before this one's MFMAs; one copy of the
   // body (rb is moved into ra, which the next iteration's MFMAs would wait for anyway)
