@@ -347,7 +347,9 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   static_assert(TN >= 2, "two W blocks in flight");
   // heads: the epilogue's constants in their own region after the W stages (R3HeadStage)
   constexpr int HS_OFF = NSTAGE * STAGE;
-  constexpr int EPI_BYTES = EPI == EPI_HEAD ? HS_OFF + R3HeadStage<NT, BN / 64>::BYTES : 2 * NW * 4;
+  // standard epilogue: the tile's winv / bias columns in LDS after the W stages (round 5: read per column
+  // block from global memory they sat behind the previous block's stores)
+  constexpr int EPI_BYTES = EPI == EPI_HEAD ? HS_OFF + R3HeadStage<NT, BN / 64>::BYTES : HS_OFF + 2 * BN * 4;
   constexpr int LDS_BYTES = NSTAGE * STAGE > EPI_BYTES ? NSTAGE * STAGE : EPI_BYTES;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
 
@@ -367,6 +369,9 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   // heads: the epilogue's constants in flight during the whole prologue (stored before its barrier)
   [[maybe_unused]] R3HeadStage<NT, BN / 64> hst;
   if constexpr (EPI == EPI_HEAD) hst.load(a, n0, nt, tid);
+  static_assert(EPI == EPI_HEAD || 2 * BN <= NT, "one winv / bias entry per thread");
+  [[maybe_unused]] const float csb_v =
+      EPI == EPI_HEAD ? 0.f : (tid < BN ? a.winv[n0 + tid] : (tid < 2 * BN && a.bias ? a.bias[n0 + tid - BN] : 0.f));
 
   // ---- A: this lane's rows (one per 16-row sub-tile), gather origins per segment ----
   // (round 5: row decomposition by multiply-high divisions, a.fd_ow / a.fd_oh from the launch)
@@ -564,6 +569,7 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   if (nk > 0) load_w(kt0, smem);
   load_a(kt0);
   if constexpr (EPI == EPI_HEAD) hst.store(reinterpret_cast<float*>(smem + HS_OFF), tid);
+  else if (tid < 2 * BN) reinterpret_cast<float*>(smem + HS_OFF)[tid] = csb_v;
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA_OPS) : "memory");
   __builtin_amdgcn_s_barrier();
   if constexpr ((ABL & 4) != 0) {
@@ -706,7 +712,8 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
                                                               ainv);
   } else {
     __syncthreads();
-    r3t_epilogue_std<TM, TN, NT, (ABL & 32768) != 0, false>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv);
+    r3t_epilogue_std<TM, TN, NT, (ABL & 32768) != 0, false, true>(a, acc, smem, m0 + wave * WM, m0, n0, lane, ainv,
+                                                                  nullptr, reinterpret_cast<const float*>(smem + HS_OFF));
   }
 }
 
