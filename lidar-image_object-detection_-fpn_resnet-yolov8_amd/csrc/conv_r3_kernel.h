@@ -369,9 +369,15 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   // heads: the epilogue's constants in flight during the whole prologue (stored before its barrier)
   [[maybe_unused]] R3HeadStage<NT, BN / 64> hst;
   if constexpr (EPI == EPI_HEAD) hst.load(a, n0, nt, tid);
-  static_assert(EPI == EPI_HEAD || 2 * BN <= NT, "one winv / bias entry per thread");
-  [[maybe_unused]] const float csb_v =
-      EPI == EPI_HEAD ? 0.f : (tid < BN ? a.winv[n0 + tid] : (tid < 2 * BN && a.bias ? a.bias[n0 + tid - BN] : 0.f));
+  constexpr int NCS = EPI == EPI_HEAD ? 1 : (2 * BN + NT - 1) / NT;  // winv / bias entries per thread
+  [[maybe_unused]] float csb_v[NCS];
+  if constexpr (EPI != EPI_HEAD) {
+#pragma unroll
+    for (int j = 0; j < NCS; ++j) {
+      const int i = tid + j * NT;
+      csb_v[j] = i < BN ? a.winv[n0 + i] : (i < 2 * BN && a.bias ? a.bias[n0 + i - BN] : 0.f);
+    }
+  }
 
   // ---- A: this lane's rows (one per 16-row sub-tile), gather origins per segment ----
   // (round 5: row decomposition by multiply-high divisions, a.fd_ow / a.fd_oh from the launch)
@@ -569,7 +575,11 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   if (nk > 0) load_w(kt0, smem);
   load_a(kt0);
   if constexpr (EPI == EPI_HEAD) hst.store(reinterpret_cast<float*>(smem + HS_OFF), tid);
-  else if (tid < 2 * BN) reinterpret_cast<float*>(smem + HS_OFF)[tid] = csb_v;
+  else {
+#pragma unroll
+    for (int j = 0; j < NCS; ++j)
+      if (tid + j * NT < 2 * BN) reinterpret_cast<float*>(smem + HS_OFF)[tid + j * NT] = csb_v[j];
+  }
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NA_OPS) : "memory");
   __builtin_amdgcn_s_barrier();
   if constexpr ((ABL & 4) != 0) {

@@ -183,8 +183,9 @@ int main(int argc, char** argv) {
       {"layer4 3x3 512->512", 16, 19, 19, 512, 512, false},
   };
   // round 5: 64 x 64 tiles at 4 blocks / CU (4 waves per SIMD) against the product 128 x 64 at 3
-  std::vector<Cand> l1 = {CS(128, 64, 32, 3, 142, 1), CS(64, 64, 16, 4, 142, 1), CS(64, 64, 16, 4, 14, 1),
-                          CS(128, 64, 32, 3, 142, 1), CS(64, 64, 16, 4, 142, 1)};
+  // (late round 5: 256-row tiles, 8 waves, 1 / 2 blocks per CU: the W tile amortised over twice the rows)
+  std::vector<Cand> l1 = {CS(128, 64, 32, 3, 142, 1), CS(256, 64, 32, 1, 142, 1), CS(256, 64, 32, 2, 142, 1),
+                          CS(128, 64, 32, 3, 142, 1), CS(256, 64, 32, 1, 142, 1), CS(256, 64, 32, 2, 142, 1)};
   // round 5: the pre-split strip (4) and the residual prefetch (128) on the 128-wide tiles
   std::vector<Cand> l2 = {CS(128, 128, 32, 2, 10, 1), CS(128, 128, 32, 2, 14, 1), CS(128, 128, 32, 2, 142, 1),
                           CS(128, 128, 32, 2, 10, 1), CS(128, 128, 32, 2, 14, 1), CS(128, 128, 32, 2, 142, 1)};
