@@ -82,8 +82,9 @@ constexpr int R3_FPN = 256 | 2048 | 32768;
 // heads: + s_setprio 1 for waves 4-7 (4), v_fma_mix split (4096), 3-block W read-ahead (8192), scalar
 // tap decode (16384), packed epilogue (65536), waves 4-7 half a K-tile behind their SIMD partners
 // with three W stages (1048576: -4.6 / -3.1 / -1.0 % per launch on L1 / L2 / L0, bit-identical,
-// profiles/r03h_convbench_heads_stagger.txt)
-constexpr int R3_HEAD_STAG = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536 | 524288 | 1048576;
+// profiles/r03h_convbench_heads_stagger.txt), the delayed half issuing every W DMA piece of the K loop
+// (2097152, round 5: -2.2 %, bit-identical, profiles/r05ah_heads_delayed_half_dma.txt)
+constexpr int R3_HEAD_STAG = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536 | 524288 | 1048576 | 2097152;
 // strip kernel (conv_h3s_kernel.h bits): transposed epilogue (2), v_fma_mix split (8), the pre-split
 // strip (4) and the residual tile loaded during the last super-step (128) on every tile shape (round
 // 5: with the one-latency presplit the 128-wide tiles gain from them too, layer2 -4.6 % / -6.5 % with a

@@ -315,6 +315,7 @@ __device__ __forceinline__ void r3t_epilogue_head(const ConvArgs& a, f32x4_t (&a
 // before the next slice: that slice (~1-2 MB per XCD for the heads) stays in the 4 MB L2, where
 // the tap-major order's whole-window working set (4-9 MB per XCD at C = 128 / 256) re-read the
 // input from the fabric at every tap (heads L0 / L1: 7x / 5x their input in HBM traffic),
+// 2097152 = (with the stagger) the delayed half issues every W DMA piece of the K loop, the leading half none,
 // 1048576 = half-tile stagger (NSTAGE 3): waves NW/2 .. NW - 1 run their K loop half a K-tile
 // behind their SIMD partners (w - NW/2). The barrier that closes interval i (W of tile i + 1
 // landed) comes after tile i for the first half of the waves and after the first half of tile i
@@ -331,7 +332,7 @@ template <int BM, int BN, int WM, int EPI, int OCC, int NSTAGE, int NSEG, int AB
 __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
   constexpr bool STAG = (ABL & 1048576) != 0;
   static_assert((ABL & (256 | 2048)) == (256 | 2048) &&
-                    (ABL & ~(4 | 256 | 2048 | 4096 | 8192 | 16384 | 32768 | 65536 | 524288 | 1048576)) == 0,
+                    (ABL & ~(4 | 256 | 2048 | 4096 | 8192 | 16384 | 32768 | 65536 | 524288 | 1048576 | 2097152)) == 0,
                 "product conv_r3 form (see the bit list)");
   static_assert(STAG ? NSTAGE == 3 : NSTAGE == 2, "W ring depth: 3 stages with the stagger, else 2");
   static_assert(NSEG == 1 || NSEG == 2, "segments");
@@ -529,6 +530,25 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) load_w_piece(j, kt, S);
   };
+  // ABL 2097152 (with the stagger; round 5): the delayed half also issues its SIMD partner's W pieces in
+  // the K loop (piece e = wave - NW / 2 + NW j), the leading half none: the delayed half (s_setprio 1)
+  // reached each barrier ~1,100 cycles early and idled there, the leading half now sheds its DMA issue
+  // (heads -2.2 %, same bits: profiles/r05ah_*)
+  constexpr bool DMA_DEL = (ABL & 2097152) != 0;
+  [[maybe_unused]] int boff_p[NB];
+  if constexpr (DMA_DEL) {
+    static_assert(NB_REM == 0, "whole pieces per wave");
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int e = (wave >= NW / 2 ? wave - NW / 2 : wave) + NW * j;
+      boff_p[j] = (int)((e / ND_BT) * term_bytes) + (e % ND_BT) * 16 * wst * 2;
+    }
+  }
+  auto load_w_piece_p = [&](int j, int kt, unsigned char* S) {
+    const int e = wave - NW / 2 + NW * j;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rsw, (__attribute__((address_space(3))) void*)(S + e * 1024), 16,
+                                             (unsigned)(wlane + boff_p[j] + 2 * kcol(kt)), 0, 0, 0);
+  };
   f16x8_t hf[2][TM];  // split A of this K-tile
   auto split_a = [&](f16x8_t (&h)[2][TM]) {
 #pragma unroll
@@ -609,7 +629,16 @@ __device__ __forceinline__ void conv_r3_body(const ConvArgs& a, int lbid) {
 #pragma unroll
       for (int jj = 0; jj < PPB; ++jj) {
         const int j = s * PPB + jj;
-        if (j < NB) load_w_piece(j, tile, S);
+        if (j < NB) {
+          if constexpr (DMA_DEL) {
+            if constexpr (HB) {
+              load_w_piece(j, tile, S);
+              load_w_piece_p(j, tile, S);
+            }
+          } else {
+            load_w_piece(j, tile, S);
+          }
+        }
       }
     };
     int st_cur = 0;

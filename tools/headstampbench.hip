@@ -82,7 +82,7 @@ static void split_weights_h3(const float* w, int N, int Kpad, uint16_t** wh, flo
 
 
 int main(int argc, char** argv) {
-  constexpr int R3_HEAD_STAG = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536 | 524288 | 1048576;  // conv.hip
+  constexpr int R3_HEAD_STAG = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536 | 524288 | 1048576 | 2097152;  // conv.hip (experiment bit)
   struct Sh { const char* name; int H, C; };
   const Sh shapes[] = {{"L0", 76, 256}, {"L1", 152, 128}, {"L2", 152, 64}};
   const int hch[5] = {3, 2, 2, 1, 3}, nhead = 5, N = 320;
