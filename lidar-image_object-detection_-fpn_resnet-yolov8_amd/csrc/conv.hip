@@ -88,9 +88,11 @@ constexpr int R3_HEAD_STAG = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536 | 5242
 // strip kernel (conv_h3s_kernel.h bits): transposed epilogue (2), v_fma_mix split (8), the pre-split
 // strip (4) and the residual tile loaded during the last super-step (128) on every tile shape (round
 // 5: with the one-latency presplit the 128-wide tiles gain from them too, layer2 -4.6 % / -6.5 % with a
-// residual, layer3 -1 / -2 %, bit-identical: profiles/r05j_*; the names of the former two forms stay)
-constexpr int H3S_64 = 2 | 4 | 8 | 128;
-constexpr int H3S_128 = 2 | 4 | 8 | 128;
+// residual, layer3 -1 / -2 %, bit-identical: profiles/r05j_*; the names of the former two forms stay),
+// the strip in registers instead of an LDS-DMA buffer (1024, late round 5: layer1 -2.7 %, layer2 -2.2 %,
+// layer4 -2.8 %, bench +0.6 %, bit-identical, profiles/r05bi_*)
+constexpr int H3S_64 = 2 | 4 | 8 | 128 | 1024;
+constexpr int H3S_128 = 2 | 4 | 8 | 128 | 1024;
 
 // FPN 1x1 convs (commuted: the low-resolution W_a . x and the skip conv with the upsampled
 // residual) on the persistent weight-resident kernel (fpn_kernel.h), by channel count.

@@ -36,6 +36,9 @@ namespace sfa {
 // into VGPRs at the step's start and written to the other W stage with ds_write_b128 after the
 // step's MFMAs (an LDS-DMA piece costs ~60 issue cycles, a load + ds_write_b128 ~20); same
 // LDS image, same products: bit-identical.
+// 1024 = (with 4; round 5) the strip into REGISTERS: each wave loads its own WM + 2 rows (the kw halo) of
+// the next (kh, chunk) strip with buffer loads at kw 1 and splits them from its VGPRs at kw 0, so the f32
+// strip never passes through LDS (no strip buffer, no LDS-DMA pieces, no f32 LDS reads in the split).
 template <int BM, int BN, int WM, int EPI, int OCC, int ABL = 0>
 __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const ConvArgs a) {
   constexpr int NW = BM / WM, NT = NW * 64;
@@ -51,14 +54,17 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
   constexpr bool PS = (ABL & 4) != 0;
   constexpr bool RESPF = PS && (ABL & 128) != 0;
   constexpr bool RW = (ABL & 256) != 0;
+  constexpr bool SREG = (ABL & 1024) != 0;
   constexpr int PROWS = WM + 2;              // a wave's pre-split rows (its WM rows + the kw halo)
   constexpr int PR_BYTES = (PROWS + 1) * 64;  // per term: 32 fp16 per row, + one zero row
-  constexpr int NSB = PS ? 1 : 2;             // f32 strip buffers
+  constexpr int NSB = PS ? (SREG ? 0 : 1) : 2;  // f32 strip buffers
+  constexpr int NP = (PROWS + 7) / 8;         // PS: pre-split row groups per wave (8 rows x 8 lanes)
   constexpr int MAIN_BYTES = NSB * S_BYTES + 2 * W_BYTES + (PS ? NW * 2 * PR_BYTES : 0);
   constexpr int CSB_OFF = MAIN_BYTES;  // the tile's winv / bias columns (epilogue), staged in the prologue
   constexpr int LDS_BYTES = MAIN_BYTES + 2 * BN * 4;
   static_assert(NW % 2 == 0 && WM % 16 == 0 && BN % 16 == 0, "tile");
-  static_assert((ABL & 10) == 10 && (ABL & ~(2 | 4 | 8 | 128 | 256)) == 0, "product strip-kernel form (see the bit list)");
+  static_assert((ABL & 10) == 10 && (ABL & ~(2 | 4 | 8 | 128 | 256 | 1024)) == 0, "product strip-kernel form (see the bit list)");
+  static_assert(!SREG || (PS && !RW), "strip in registers: the pre-split form, W by LDS-DMA");
   static_assert(EPI == EPI_STD, "transposed form: standard epilogue only");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS_BYTES];
 
@@ -114,6 +120,22 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
   }
   auto swzP = [](int R) { return ((R >> 2) & 1) << 1; };  // conflict-free at every kw row offset
 
+  // SREG: this lane's pre-split rows r = 8 p + lane / 8 of the wave (strip row wave WM + r, input pixel
+  // m0 - 1 + wave WM + r), channels 4 (lane & 7) .. + 3 of the chunk: byte offset and kh validity bits
+  [[maybe_unused]] int p_base[NP];
+  [[maybe_unused]] unsigned p_ok = 0;
+  if constexpr (SREG) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int r = 8 * p + (lane >> 3);
+      const int m = m0 - 1 + wave * WM + r;
+      const bool ok = r < PROWS && m >= 0 && m < M;
+      const int t = fast_div(ok ? m : 0, a.fd_w);
+      const int y = t - fast_div(t, a.fd_h) * H;
+      p_base[p] = ((m << g.logC) + 4 * (lane & 7)) << 2;
+      p_ok |= ok ? ((y > 0 ? 1u : 0u) | 2u | (y < H - 1 ? 4u : 0u)) << (3 * p) : 0u;
+    }
+  }
   const int lognchunk = g.logC - 5, nchunk = 1 << lognchunk;
   const int nsl = 3 * nchunk / nsplit;  // this block's (kh, chunk) super-steps s0 .. s0 + nsl - 1
   const int s0 = kz * nsl;
@@ -128,6 +150,17 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
             rsx, (__attribute__((address_space(3))) void*)(S + (wave + NW * i) * 1024), 16, off, 0, 0, 0);
       }
+    }
+  };
+  [[maybe_unused]] x6_f32x4 xs[NP];  // SREG: the next strip's rows
+  auto load_strip_regs = [&](int s) {
+    const int kh = s >> lognchunk, c0 = (s & (nchunk - 1)) << 5;
+    const int delta = ((((kh - 1) * W) << g.logC) + c0) << 2;  // uniform
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const bool ok = (p_ok >> (3 * p + kh)) & 1u;
+      const unsigned off = ok ? (unsigned)(p_base[p] + delta) : 0x80000000u;
+      xs[p] = __builtin_bit_cast(x6_f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsx, off, 0, 0));
     }
   };
   auto load_w = [&](int k0, unsigned char* S) {
@@ -209,12 +242,12 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     const int rr = lane >> 3, q = lane & 7;
     // every row's read first: one LDS latency, not one per row (the compiler cannot tell the strip
     // reads from the pre-split writes apart and waits after each read otherwise; profiles/r05g_*)
-    constexpr int NP = (PROWS + 7) / 8;
     x6_f32x4 xr[NP];
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       const int r = 8 * p + rr, j = wave * WM + (r < PROWS ? r : 0);
-      xr[p] = *reinterpret_cast<const x6_f32x4*>(Ss + j * AROW + ((q ^ swzA(j)) << 4));
+      if constexpr (SREG) xr[p] = xs[p];
+      else xr[p] = *reinterpret_cast<const x6_f32x4*>(Ss + j * AROW + ((q ^ swzA(j)) << 4));
     }
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
@@ -297,6 +330,9 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
     load_strip(s0, smem);
     wait_w_regs(1);
     store_w_regs(WB);
+  } else if constexpr (SREG) {
+    load_strip_regs(s0);
+    load_w(wk0(s0, 0), WB);
   } else {
     load_strip(s0, smem);
     load_w(wk0(s0, 0), WB);
@@ -315,7 +351,9 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
               asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TM * TN) : "memory");
             else
               asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          } else if (NS_REM == 0 || wave < NS_REM)
+          } else if (SREG)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NP) : "memory");
+          else if (NS_REM == 0 || wave < NS_REM)
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS) : "memory");
           else
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NS - 1) : "memory");
@@ -333,7 +371,8 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
           if (RESPF && last) {  // the residual tile (the last MFMAs hide its latency)
             if (a.res && nsplit == 1) r3t_res_load<TM, TN>(a, rvp, m0 + wave * WM, n0, lane);
           } else {
-            load_strip(last ? s : s + 1, smem);  // every wave has split strip s
+            if constexpr (SREG) load_strip_regs(last ? s : s + 1);  // this wave has split strip s
+            else load_strip(last ? s : s + 1, smem);                 // every wave has split strip s
             strip_after = true;
           }
         }
