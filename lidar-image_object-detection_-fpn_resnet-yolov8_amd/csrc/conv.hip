@@ -93,6 +93,9 @@ constexpr int R3_HEAD_STAG = 256 | 2048 | 4 | 4096 | 8192 | 16384 | 65536 | 5242
 // layer4 -2.8 %, bench +0.6 %, bit-identical, profiles/r05bi_*)
 constexpr int H3S_64 = 2 | 4 | 8 | 128 | 1024;
 constexpr int H3S_128 = 2 | 4 | 8 | 128 | 1024;
+// 128 x 128 tiles (layer2): at 3 blocks / CU without the residual prefetch (198 -> 168 VGPRs; the strip in
+// registers freed the LDS), 722 tiles in one round of 768 slots: -1.9 %, bit-identical, profiles/r05bj_*
+constexpr int H3S_128W = 2 | 4 | 8 | 1024;
 
 // FPN 1x1 convs (commuted: the low-resolution W_a . x and the skip conv with the upsampled
 // residual) on the persistent weight-resident kernel (fpn_kernel.h), by channel count.
@@ -162,7 +165,7 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
       // same bits (tools/convbench4: 102.4-105.0 vs 107.4-110.7 us, profiles/r04o_convbench4_layer4_splits.txt)
       rc = launch_conv_h3s_cfg<128, 64, 32, EPI_STD, 3, H3S_64>(b, st);
     else if (strip && (3 * (a.seg[0].C >> 5)) % b.ksplit == 0)
-      rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 2, H3S_128>(b, st);
+      rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 3, H3S_128W>(b, st);
     else if (!strip && tile_rows(a) >= 50000)  // big-M stride-2 / two-segment: A from registers
       rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
     if (!ok(rc)) {
