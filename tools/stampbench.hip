@@ -158,7 +158,7 @@ int main(int argc, char** argv) {
     for (int it = 0; it < 3; ++it) {  // warm (caches, clocks), the last launch's stamps are kept
       if (sh.N == 64) rc = launch_conv_h3s_stamp_cfg<128, 64, 32, EPI_STD, 3, 1166>(a, st);
       else if (sh.N == 512) rc = launch_conv_h3s_stamp_cfg<128, 64, 32, EPI_STD, 3, 1166>(a, st);
-      else rc = launch_conv_h3s_stamp_cfg<128, 128, 32, EPI_STD, 2, 1166>(a, st);
+      else rc = launch_conv_h3s_stamp_cfg<128, 128, 32, EPI_STD, 3, 1038>(a, st);
       if (rc != SFA_OK) { printf("%s: launch failed\n", sh.name); return 1; }
     }
     CK(hipStreamSynchronize(st));
