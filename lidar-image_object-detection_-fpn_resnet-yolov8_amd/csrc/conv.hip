@@ -171,7 +171,12 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     if (!ok(rc)) {
       b.tile_cnt = nullptr;  // conv_h3: the reduce launch (conv_h3_kernel.h splitk_ticket)
       if ((a.Kpad / 32) % b.ksplit != 0) b.ksplit = 1;  // K not divisible into the slices: no split
-      rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2, 1>(b, st);
+      // the FPN low-resolution 1x1 convs left on conv_h3 (level 1's at mask 61): 64 x 128 tiles, 2 x 2 waves,
+      // 3 blocks / CU, same K order (late round 5: 23.4 -> 18.0 us, bit-identical, profiles/r05bo_*; the
+      // layer3 / 4 convs on the same tiles were slower, r05bn_*)
+      if (sliced && a.seg[0].KH == 1 && a.seg[0].KW == 1)
+        rc = launch_conv_h3_cfg<64, 128, 32, EPI_STD, 3, 32, 2, false, 2, 1, 64>(b, st);
+      if (!ok(rc)) rc = launch_conv_h3_cfg<128, 128, 32, EPI_STD, 2, 32, 2, false, 2, 1>(b, st);
     }
     if (!ok(rc) && !sliced) rc = launch_conv_x6g_cfg<128, 128, 32, EPI_STD, 2, 16, 3, 0, 128, 1>(b, st);
   }
