@@ -167,7 +167,9 @@ static int launch_conv_h3(const ConvArgs& a, int epilogue, hipStream_t st) {
     else if (strip && (3 * (a.seg[0].C >> 5)) % b.ksplit == 0)
       rc = launch_conv_h3s_cfg<128, 128, 32, EPI_STD, 3, H3S_128W>(b, st);
     else if (!strip && tile_rows(a) >= 50000)  // big-M stride-2 / two-segment: A from registers
-      rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 2, 2, R3_BODY>(b, st);
+      // (3 blocks / CU, late round 5: 150-153 VGPRs, 722 tiles in one round; per launch within 1 %, bench
+      // +0.9 % with two steps in flight, bit-identical: profiles/r05bp_*)
+      rc = launch_conv_r3_cfg<128, 128, 32, EPI_STD, 3, 2, R3_BODY>(b, st);
     if (!ok(rc)) {
       b.tile_cnt = nullptr;  // conv_h3: the reduce launch (conv_h3_kernel.h splitk_ticket)
       if ((a.Kpad / 32) % b.ksplit != 0) b.ksplit = 1;  // K not divisible into the slices: no split
