@@ -109,8 +109,15 @@ def parse(argv=None):
                     help="N > 1: the detections' all-gather on each step's own stream, or on one "
                          "extra stream")
     ap.add_argument("--sim-gather", action="store_true",
-                    help="N = 1: a device copy of the detections where the all-gather would go "
-                         "(rehearses the N > 1 stream layout on one GPU)")
+                    help="N = 1: rehearse the N > 1 layout on one GPU: the models without side "
+                         "streams (side_streams_for) and, where the all-gather goes, a device copy of "
+                         "the detections enqueued the way torch's RCCL process group enqueues a "
+                         "collective (its own stream, created on first use, joined to the step's stream "
+                         "before and after)")
+    ap.add_argument("--dump-dets", default=None, metavar="NPZ",
+                    help="after the timed region, every pipeline runs one more step and rank 0 writes "
+                         "the gathered detections (nf, world*B, K, 10), frame ids (nf, world*B) and each "
+                         "rank's input seed to NPZ (tests/test_gpu_bench_multirank.py)")
     ap.add_argument("--share-weights", action="store_true",
                     help="the in-flight pipelines share one device copy of the packed weights "
                          "(KfpnEngine.twin) instead of one copy each")
@@ -136,7 +143,8 @@ def side_streams_for(args, world, nf):
     queues, so "auto" keeps them only while the pipelines' streams and theirs fit (N = 1, at
     most 2 pipelines); RCCL's own stream at N > 1 and a third pipeline do not
     (profiles/r02b_ab_gather_streams.txt, r02c_ab_fusion_inflight3.txt)."""
-    return {"on": True, "off": False, "auto": world == 1 and nf <= 2}[args.side_streams]
+    return {"on": True, "off": False,
+            "auto": world == 1 and not getattr(args, "sim_gather", False) and nf <= 2}[args.side_streams]
 
 
 def _free_port() -> int:
@@ -393,12 +401,16 @@ class BevInferBench:
                 p.engine.set_probe(_lib.PROBE_SERIAL)
         self.steps = [StepGraphs(p, not args.no_graph) for p in pipes]
         self.streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nf - 1)]
-        # --sim-gather (N = 1): a device copy of the detections in place of the all-gather, on the
-        # same stream the gather would use (the N > 1 stream layout rehearsed on one GPU)
+        # --sim-gather (N = 1): a device copy of the detections in place of the all-gather, on a
+        # stream of its own joined to the step's stream as ProcessGroupNCCL joins its RCCL stream
+        # (the N > 1 stream layout rehearsed on one GPU)
         self.gather = world > 1 or args.sim_gather
+        self.last_gathered = [None] * nf
         if self.gather:
             self.frame_ids = torch.arange(rank * args.batch, (rank + 1) * args.batch, device=dev)
-            self.sim_out = torch.empty_like(pipes[0].dets)
+            self.sim_out = torch.empty((world * args.batch,) + tuple(pipes[0].dets.shape[1:]),
+                                       dtype=torch.float32, device=dev)
+            self.sim_stream = None
         self.comm_mode = self.gather and args.gather_stream == "comm"
         if self.comm_mode:
             # all-gathers on one extra stream in step order (the same collective order on every
@@ -411,9 +423,15 @@ class BevInferBench:
     def do_gather(self, dets):
         if self.world > 1:
             from sfa_hip import dist as sdist
-            sdist.gather_detections(dets, self.frame_ids)
-        else:
+            return sdist.gather_detections(dets, self.frame_ids)
+        cur = torch.cuda.current_stream()
+        if self.sim_stream is None:  # created on first use, after every pipeline's streams
+            self.sim_stream = torch.cuda.Stream()
+        self.sim_stream.wait_stream(cur)
+        with torch.cuda.stream(self.sim_stream):
             self.sim_out.copy_(dets)
+        cur.wait_stream(self.sim_stream)
+        return self.sim_out, self.frame_ids
 
     def one_step(self, k, ev=None):
         i = k % self.nf
@@ -433,13 +451,30 @@ class BevInferBench:
             elif self.gather:
                 # on the step's own stream, in step order (the same collective order on every
                 # rank); RCCL's stream waits for this step only, the other pipeline runs on
-                self.do_gather(self.pipes[i].dets)
+                self.last_gathered[i] = self.do_gather(self.pipes[i].dets)
         if self.comm_mode:
             with torch.cuda.stream(self.comm):
                 self.comm.wait_event(self.step_done[i])
-                self.do_gather(self.pipes[i].dets)
+                self.last_gathered[i] = self.do_gather(self.pipes[i].dets)
                 self.comm_done[i].record()
             self.gathered[i] = 1
+
+
+def dump_gathered(args, bench, rank, world):
+    """--dump-dets: one more step per pipeline after the timed region (every rank, so the
+    collectives pair up); rank 0 writes what each step's gather returned."""
+    dets, ids, local = [], [], []
+    for i in range(bench.nf):
+        bench.one_step(i)
+        torch.cuda.synchronize()
+        d, fid = bench.last_gathered[i] if bench.gather else (bench.pipes[i].dets, None)
+        dets.append(d.cpu().numpy())
+        ids.append(fid.cpu().numpy() if fid is not None else np.arange(args.batch, dtype=np.int64))
+        local.append(bench.pipes[i].dets.cpu().numpy())
+    if rank == 0:
+        np.savez(args.dump_dets, dets=np.stack(dets), ids=np.stack(ids), local=np.stack(local),
+                 input_seed=np.array([1 + r for r in range(world)], np.int64), world=np.int64(world),
+                 side_streams=np.int64(bench.side))
 
 
 def traffic_per_forward(args):
@@ -879,6 +914,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if args.dump_dets:
+        dump_gathered(args, bench, rank, world)
     if nf > 1:
         # per-stage times with one step in flight (the in-flight events overlap): a short
         # untimed-for-value pass on stream 0 only, for the roofline and stages_ms
@@ -938,6 +975,9 @@ def main():
                 "hip_graph": not args.no_graph,
                 "steps_in_flight": nf,
                 "side_streams": side,
+                "gather": ("RCCL all_gather_into_tensor of the (B, K, 10) detections + frame ids per step"
+                           if world > 1 else "simulated: device copy on a lazily created stream joined "
+                           "like ProcessGroupNCCL's (--sim-gather)" if args.sim_gather else None),
             },
             "stages_ms": {"forward": round(fwd_ms, 4), "decode": round(dec_ms, 4),
                           "note": "one step in flight; value/ms_per_step use %d in flight" % nf},

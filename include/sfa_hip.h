@@ -204,8 +204,15 @@ int sfa_model_probe_times(const sfa_model* model, float* ms, int n);
  * utils/demo_utils.py:110-111 do_detect, fused into the layout conversion.
  * H, W multiples of 32.  head_out[i]: device float32 (B, c_i, H/4, W/4) NCHW,
  * contiguous, forward head order — raw logits like the reference (no sigmoid).
- * workspace: sfa_forward_workspace_size(B, H, W) bytes. */
+ * workspace: sfa_forward_workspace_size(B, H, W) bytes.
+ * Batch limit: the conv kernels address each input map with 32-bit byte offsets, so one pass
+ * holds at most sfa_forward_max_batch(H, W) frames = floor((2^31 - 1) / (32 H W)) (the widest
+ * conv input, up_level3, is 32 H W bytes per frame): 181 frames at 608 x 608.  A larger batch
+ * runs as consecutive passes of that many frames on the caller's stream, sharing one workspace
+ * sized for a pass (bit-identical per frame: the arithmetic is batch-invariant); a single frame
+ * too large for one pass (H W >= 2^26) is refused with SFA_E_UNSUPPORTED before any launch. */
 enum sfa_input_layout { SFA_IN_NCHW3 = 0, SFA_IN_NHWC4 = 1, SFA_IN_NCHW3_FLIP_HW = 2 };
+int sfa_forward_max_batch(int height, int width);
 size_t sfa_forward_workspace_size(const sfa_model* model, int batch, int height, int width);
 int sfa_model_forward(const sfa_model* model, const float* x, int in_layout, int batch, int height,
                       int width, float* const* head_out, void* workspace, size_t workspace_bytes,

@@ -665,15 +665,35 @@ static ConvArgs conv_args(const float* wbase, const PConv& pc, int B, int OH, in
 
 }  // namespace sfa
 
+// Frames one forward pass runs at once (sfa_forward_max_batch): every conv kernel reads its input
+// segments through buffer resources with 32-bit byte offsets (conv.hip launch_conv: < 2 GiB). The
+// widest conv input per frame is up_level3 / the level-1 heads' input, (H/4)(W/4) x 128 floats =
+// 32 H W bytes (the stem input, 12-16 H W bytes, and every other map are smaller), so a pass holds
+// floor((2^31 - 1) / (32 H W)) frames: 181 at 608 x 608. Larger batches run in passes of that
+// many frames (sfa_model_forward); frames are independent and their arithmetic batch-invariant
+// (per-frame fp16x3 scales), so the chunking changes no bit.
+static int forward_max_batch(int H, int W) {
+  if (H <= 0 || W <= 0) return 0;
+  const unsigned long long per_frame = 32ull * (unsigned long long)H * (unsigned long long)W;
+  const unsigned long long n = ((1ull << 31) - 1) / per_frame;
+  return n > 0x7fffffffull ? 0x7fffffff : (int)n;
+}
+
+extern "C" int sfa_forward_max_batch(int height, int width) { return forward_max_batch(height, width); }
+
 extern "C" size_t sfa_forward_workspace_size(const sfa_model* m, int batch, int height, int width) {
   if (!m || batch <= 0 || height <= 0 || width <= 0) return 0;
-  return plan_bufs(&m->arch, batch, height, width).total;
+  const int bmax = forward_max_batch(height, width);
+  if (bmax < 1) return 0;
+  return plan_bufs(&m->arch, std::min(batch, bmax), height, width).total;
 }
 
 extern "C" int64_t sfa_forward_buffer_offset(const sfa_model* m, int batch, int height, int width,
                                              int which) {
   if (!m || batch <= 0 || height <= 0 || width <= 0) return -1;
-  const Bufs b = plan_bufs(&m->arch, batch, height, width);
+  const int bmax = forward_max_batch(height, width);
+  if (bmax < 1) return -1;
+  const Bufs b = plan_bufs(&m->arch, std::min(batch, bmax), height, width);
   switch (which) {
     case SFA_BUF_LAYER1: return (int64_t)b.l[0];
     case SFA_BUF_LAYER2: return (int64_t)b.l[1];
@@ -695,22 +715,10 @@ extern "C" int64_t sfa_forward_buffer_offset(const sfa_model* m, int batch, int 
     if (rc_ != SFA_OK) return rc_; \
   } while (0)
 
-extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layout, int B, int H,
-                                 int W, float* const* head_out, void* workspace,
-                                 size_t workspace_bytes, void* stream) {
-  SFA_CHECK_ARG(m && x && head_out && workspace, "forward: null argument");
-  SFA_CHECK_ARG(B >= 1 && H >= 32 && W >= 32 && H % 32 == 0 && W % 32 == 0,
-                "forward: input (%d, 3, %d, %d) must have H, W multiples of 32", B, H, W);
-  SFA_CHECK_ARG(in_layout == SFA_IN_NCHW3 || in_layout == SFA_IN_NHWC4 ||
-                    in_layout == SFA_IN_NCHW3_FLIP_HW,
-                "forward: bad layout");
-  SFA_CHECK_ARG((long long)B * H * W * 4 < (1ll << 31), "forward: input too large");
+// One pass over B <= forward_max_batch(H, W) frames (arguments checked by sfa_model_forward).
+static int forward_pass(const sfa_model* m, const float* x, int in_layout, int B, int H, int W,
+                        float* const* head_out, void* workspace, void* stream) {
   const Bufs bf = plan_bufs(&m->arch, B, H, W);
-  if (workspace_bytes < bf.total) {
-    set_error("forward: workspace %zu < required %zu bytes", workspace_bytes, bf.total);
-    return SFA_E_WORKSPACE;
-  }
-  for (int j = 0; j < m->arch.num_heads; ++j) SFA_CHECK_ARG(head_out[j], "forward: null head out");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   char* ws = reinterpret_cast<char*>(workspace);
   auto F = [&](size_t off) { return reinterpret_cast<float*>(ws + off); };
@@ -1001,5 +1009,40 @@ extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layo
   ko.num_heads = m->arch.num_heads;
   ko.total_ch = nch;
   SFA_RC(launch_kfpn(F(bf.L0), F(bf.L1), F(bf.L2), ko, B, H4, W4, st));
+  return SFA_OK;
+}
+
+extern "C" int sfa_model_forward(const sfa_model* m, const float* x, int in_layout, int B, int H,
+                                 int W, float* const* head_out, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
+  SFA_CHECK_ARG(m && x && head_out && workspace, "forward: null argument");
+  SFA_CHECK_ARG(B >= 1 && H >= 32 && W >= 32 && H % 32 == 0 && W % 32 == 0,
+                "forward: input (%d, 3, %d, %d) must have H, W multiples of 32", B, H, W);
+  SFA_CHECK_ARG(in_layout == SFA_IN_NCHW3 || in_layout == SFA_IN_NHWC4 ||
+                    in_layout == SFA_IN_NCHW3_FLIP_HW,
+                "forward: bad layout");
+  const int bmax = forward_max_batch(H, W);
+  if (bmax < 1) {
+    set_error("forward: one %d x %d frame exceeds the conv kernels' 32-bit buffer offsets", H, W);
+    return SFA_E_UNSUPPORTED;
+  }
+  const int bc = std::min(B, bmax);
+  const size_t need = plan_bufs(&m->arch, bc, H, W).total;
+  if (workspace_bytes < need) {
+    set_error("forward: workspace %zu < required %zu bytes", workspace_bytes, need);
+    return SFA_E_WORKSPACE;
+  }
+  for (int j = 0; j < m->arch.num_heads; ++j) SFA_CHECK_ARG(head_out[j], "forward: null head out");
+  // batches above the per-pass limit run as consecutive passes of bc frames on the caller's stream,
+  // sharing the workspace (stream order serialises them)
+  const size_t in_frame = (size_t)(in_layout == SFA_IN_NHWC4 ? 4 : 3) * H * W;
+  const size_t out_px = (size_t)(H / 4) * (W / 4);
+  float* outs[SFA_MAX_HEADS];
+  for (int f0 = 0; f0 < B; f0 += bc) {
+    const int nb = std::min(bc, B - f0);
+    for (int j = 0; j < m->arch.num_heads; ++j)
+      outs[j] = head_out[j] + (size_t)f0 * m->arch.head_channels[j] * out_px;
+    SFA_RC(forward_pass(m, x + (size_t)f0 * in_frame, in_layout, nb, H, W, outs, workspace, stream));
+  }
   return SFA_OK;
 }

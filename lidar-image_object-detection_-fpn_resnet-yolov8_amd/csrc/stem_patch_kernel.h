@@ -746,6 +746,10 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
     // reaches 2 GiB run in frame chunks (the side-buffer slots keep their global tile index)
     const size_t fbytes = (size_t)(a.stem_in == STEM_IN_NHWC4 ? 4 : 3) * g.H * g.W * 4;
     const int fchunk = (int)std::min<size_t>((size_t)frames, ((1ull << 31) - 1) / fbytes);
+    if (fchunk < 1) {
+      set_error("stem_patch: one %d x %d frame exceeds the 32-bit buffer offsets", g.H, g.W);
+      return SFA_E_UNSUPPORTED;
+    }
     const int tpf = (a.OH / 16) * (a.OW / 16);
     for (int f0 = 0; f0 < frames; f0 += fchunk) {
       const int nf = std::min(fchunk, frames - f0);
@@ -765,6 +769,7 @@ inline int launch_stem_patch_pool(const ConvArgs& a, hipStream_t st) {
           break;
         default: hipLaunchKernelGGL((stem_patch_pool2_kernel<STEM_IN_NHWC4, 1>), gc, bd, 0, st, c, nt); break;
       }
+      SFA_LAUNCH_CHECK();
     }
   } else if (a.stem_in == STEM_IN_NCHW3) {
     hipLaunchKernelGGL((stem_patch_pool_kernel<0, STEM_IN_NCHW3>), gd, bd, 0, st, a, ntiles);

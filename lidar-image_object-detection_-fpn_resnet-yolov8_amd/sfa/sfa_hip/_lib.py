@@ -66,6 +66,7 @@ _PROTOS = {
     "sfa_pack_weights": (_c_int, [ctypes.POINTER(SfaArch), _vp, _c_size, _vp]),
     "sfa_model_create": (_c_int, [ctypes.POINTER(SfaArch), _vp, ctypes.POINTER(_vp)]),
     "sfa_model_destroy": (None, [_vp]),
+    "sfa_forward_max_batch": (_c_int, [_c_int, _c_int]),
     "sfa_forward_workspace_size": (_c_size, [_vp, _c_int, _c_int, _c_int]),
     "sfa_forward_buffer_offset": (_c_i64, [_vp, _c_int, _c_int, _c_int, _c_int]),
     "sfa_model_forward": (_c_int, [_vp, _vp, _c_int, _c_int, _c_int, _c_int, ctypes.POINTER(_vp),

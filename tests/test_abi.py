@@ -223,3 +223,34 @@ def test_workspace_sizes():
     L = _lib.lib()
     assert L.sfa_decode_workspace_size(16, 3, 50) >= 16 * 3 * 50 * 8
     assert L.sfa_filter_scratch_size(132880) >= 4 * ((132880 + 2047) // 2048)
+
+
+def test_forward_batch_limit():
+    """include/sfa_hip.h batch limit: one pass holds floor((2^31 - 1) / (32 H W)) frames (the conv
+    kernels' 32-bit buffer offsets; up_level3 is the widest conv input), 181 at 608 x 608; the
+    workspace is sized for one pass; a frame too large for any pass is refused before a launch."""
+    L = _lib.lib()
+    assert L.sfa_forward_max_batch(608, 608) == 181
+    assert L.sfa_forward_max_batch(608, 608) == ((1 << 31) - 1) // (32 * 608 * 608)
+    assert L.sfa_forward_max_batch(96, 96) == ((1 << 31) - 1) // (32 * 96 * 96)
+    assert L.sfa_forward_max_batch(8192, 8192) == 0 and L.sfa_forward_max_batch(0, 608) == 0
+    arch = _lib.make_arch(gc.HEADS)
+    ws = ctypes.create_string_buffer(16)
+    p = ctypes.cast(ws, ctypes.c_void_p)
+    h = ctypes.c_void_p()
+    assert L.sfa_model_create(ctypes.byref(arch), p, ctypes.byref(h)) == 0
+    try:
+        one = L.sfa_forward_workspace_size(h, 181, 608, 608)
+        assert one > 0 and L.sfa_forward_workspace_size(h, 182, 608, 608) == one
+        assert L.sfa_forward_workspace_size(h, 1000, 608, 608) == one
+        assert L.sfa_forward_workspace_size(h, 180, 608, 608) < one
+        assert L.sfa_forward_workspace_size(h, 1, 8192, 8192) == 0
+        assert L.sfa_forward_buffer_offset(h, 1000, 608, 608, 0) == L.sfa_forward_buffer_offset(h, 181, 608, 608, 0)
+        outs = (ctypes.c_void_p * arch.num_heads)(*([p.value] * arch.num_heads))
+        # H = W = 8192: one frame's up_level3 alone is 2 GiB -> SFA_E_UNSUPPORTED, no launch
+        assert L.sfa_model_forward(h, p, _lib.IN_NCHW3, 1, 8192, 8192, outs, p, 1 << 40, None) == -2
+        assert b"32-bit buffer offsets" in L.sfa_last_error_string()
+        # a workspace sized for fewer frames than one pass is refused (SFA_E_WORKSPACE)
+        assert L.sfa_model_forward(h, p, _lib.IN_NCHW3, 200, 608, 608, outs, p, one - 1, None) == -4
+    finally:
+        L.sfa_model_destroy(h)

@@ -1,6 +1,6 @@
 # Same-box A/B of the in-tree library against a previous build (run on the GPU box), the form of every
 # round-5 kernel change (profiles/r05*):
-#   cp <pkg>/sfa/sfa_hip/libsfa_hip.so tools/experiments/r05/libsfa_hip_prev.so   # before the change, here
+#   cp <pkg>/sfa/sfa_hip/libsfa_hip.so tools/prev_lib/libsfa_hip_prev.so   # before the change, here
 #   <edit, build>                                                                  # then
 #   gpurun -- 'bash tools/ab_lib.sh TAG "KERNEL_REGEX" [stamps,hstamps,tests,bits,ab,prof]'
 # Parts (default all but stamps / hstamps): tests = the model + timed-config parity GPU tests; bits =
@@ -14,7 +14,7 @@ TAG="$1"
 RX="${2:-conv_}"
 PARTS=",${3:-tests,bits,ab,prof},"
 has() { [[ "$PARTS" == *",$1,"* ]]; }
-PREV=tools/experiments/r05/libsfa_hip_prev.so
+PREV=tools/prev_lib/libsfa_hip_prev.so
 NEW=lidar-image_object-detection_-fpn_resnet-yolov8_amd/sfa/sfa_hip/libsfa_hip.so
 if has stamps; then
   timeout -k 10 120 ./tools/stampbench > gpurun_out/${TAG}_stampbench.txt 2>&1 || { echo "stampbench failed"; exit 1; }
