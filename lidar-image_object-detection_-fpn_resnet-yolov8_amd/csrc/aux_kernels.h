@@ -21,5 +21,10 @@ int launch_upsample2x(const float* x, float* y, int B, int H, int W, int C, hipS
 int launch_kfpn(const float* L0, const float* L1, const float* L2, const KfpnOut& o, int B, int h,
                 int w, hipStream_t st);
 int launch_sigmoid_clamp(float* x, long long n, hipStream_t st);
+// Zero `bytes` (a multiple of 4, 4-B aligned) of device memory with a kernel instead of
+// hipMemsetAsync: on this ROCm a memset captured into a single-branch HIP graph is replayed from a
+// kernel-argument slot that later launches reuse, so the replayed node zeroes whatever that slot
+// then points at (tools/debug/graph_repro.py); kernel nodes keep their own arguments.
+int launch_zero_words(void* p, size_t bytes, hipStream_t st);
 
 }  // namespace sfa

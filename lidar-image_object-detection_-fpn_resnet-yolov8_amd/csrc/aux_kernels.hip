@@ -273,6 +273,42 @@ int launch_kfpn(const float* L0, const float* L1, const float* L2, const KfpnOut
   return SFA_OK;
 }
 
+__global__ void zero_words_kernel(uint4* __restrict__ p4, long long n4, unsigned* __restrict__ tail, int ntail) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n4) p4[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (i < ntail) tail[i] = 0u;
+}
+
+int launch_zero_words(void* p, size_t bytes, hipStream_t st) {
+  if (bytes == 0) return SFA_OK;
+  if (!p || (bytes & 3) || (reinterpret_cast<uintptr_t>(p) & 3)) {
+    set_error("zero_words: %zu bytes at %p (need 4-B multiples, 4-B aligned)", bytes, p);
+    return SFA_E_INVALID;
+  }
+  // 16-B stores up to the first 16-B boundary's multiple, words for the rest
+  char* c = reinterpret_cast<char*>(p);
+  const size_t head = (16 - (reinterpret_cast<uintptr_t>(c) & 15)) & 15;
+  if (head >= bytes || bytes - head < 16) {
+    const long long nw = (long long)(bytes / 4);
+    hipLaunchKernelGGL(zero_words_kernel, dim3(grid_of(nw)), dim3(256), 0, st, nullptr, 0ll,
+                       reinterpret_cast<unsigned*>(c), (int)nw);
+    SFA_LAUNCH_CHECK();
+    return SFA_OK;
+  }
+  const long long n4 = (long long)((bytes - head) / 16);
+  if (head) {  // the few words before the 16-B boundary (one extra launch only for unaligned starts)
+    hipLaunchKernelGGL(zero_words_kernel, dim3(1), dim3(256), 0, st, nullptr, 0ll, reinterpret_cast<unsigned*>(c),
+                       (int)(head / 4));
+    SFA_LAUNCH_CHECK();
+  }
+  const size_t done = head + (size_t)n4 * 16;
+  hipLaunchKernelGGL(zero_words_kernel, dim3(grid_of(n4 > 64 ? n4 : 64)), dim3(256), 0, st,
+                     reinterpret_cast<uint4*>(c + head), n4, reinterpret_cast<unsigned*>(c + done),
+                     (int)((bytes - done) / 4));
+  SFA_LAUNCH_CHECK();
+  return SFA_OK;
+}
+
 int launch_sigmoid_clamp(float* x, long long n, hipStream_t st) {
   if (n <= 0) return SFA_OK;
   hipLaunchKernelGGL(sigmoid_clamp_kernel, dim3(grid_of(n)), dim3(256), 0, st, x, n);

@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "aux_kernels.h"
 #include "common.h"
 
 namespace sfa {
@@ -841,8 +842,7 @@ extern "C" int sfa_filter_points(const float* points, int64_t n_points, const do
   int* bcount = reinterpret_cast<int*>(scratch);
   const float4* p4 = reinterpret_cast<const float4*>(points);
   if (nb == 0) {
-    SFA_HIP_TRY(hipMemsetAsync(out_count, 0, sizeof(int64_t), st));
-    return SFA_OK;
+    return launch_zero_words(out_count, sizeof(int64_t), st);  // a kernel node, not a memset (aux_kernels.h)
   }
   hipLaunchKernelGGL(filter_count_kernel, dim3(nb), dim3(kFiltThreads), 0, st, p4,
                      (long long)n_points, f, bcount);

@@ -732,7 +732,7 @@ static int forward_pass(const sfa_model* m, const float* x, int in_layout, int B
   };
   auto blk_slot = [](int li, int bi, int ci) { return AM_BLK + 4 * li + 2 * bi + ci; };
   if (h3)  // the amax words and the split-K tickets after them
-    SFA_HIP_TRY(hipMemsetAsync(ws + bf.amax, 0, bf.tick + 4 * bf.tick_words * 4 - bf.amax, st));
+    SFA_RC(launch_zero_words(ws + bf.amax, bf.tick + 4 * bf.tick_words * 4 - bf.amax, st));
   auto io = [&](ConvArgs& a, int in0, int in1, int out) {
     a.amax_in[0] = in0 >= 0 ? AM(in0) : nullptr;
     a.amax_in[1] = in1 >= 0 ? AM(in1) : nullptr;

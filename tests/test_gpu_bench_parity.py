@@ -33,11 +33,11 @@ def _oracle_sd():
     return model_oracle.state_dict_torch(synthetic.synthetic_state_dict(_lib.state_layout(arch), seed=0))
 
 
-def _run_timed_config(argv, gpu, steps=4):
+def _run_timed_config(argv, gpu, steps=4, side=True):
     args = bench.parse(argv)
     assert args.batch == 16 and args.inflight == 2 and args.math == "fp16x3" and not args.no_graph
     b = bench.BevInferBench(args, 0, 1, gpu)
-    assert b.nf == 2 and b.side is True and all(s.graphs is not None for s in b.steps)
+    assert b.nf == 2 and b.side is side and all(s.graphs is not None for s in b.steps)
     for k in range(steps):
         b.one_step(k)
     torch.cuda.synchronize()
@@ -89,6 +89,16 @@ def test_bench_bev_infer_config_matches_oracle(gpu):
     print("bench bev_infer config: max rel logit err per pipeline", errs)
     ferrs = [_check_full_identity(p, ref, args.K) for p in b.pipes]
     print("bench bev_infer config: max abs det err vs the oracle forward's decode", ferrs)
+    # the N > 1 stream layout (configs[3]) rehearsed on one GPU: side streams off, the gather's
+    # stand-in on a stream of its own joined like ProcessGroupNCCL's (single-branch graphs: the
+    # layout whose replays the graph-captured memset broke, tests/test_gpu_graphs.py)
+    del b
+    torch.cuda.empty_cache()
+    args, b = _run_timed_config(["--sim-gather"], gpu, steps=6, side=False)
+    errs = [_check_pipe(p, ref, args.K) for p in b.pipes]
+    ferrs = [_check_full_identity(p, ref, args.K) for p in b.pipes]
+    np.testing.assert_array_equal(b.sim_out.cpu().numpy(), b.pipes[1].dets.cpu().numpy())
+    print("bench N > 1 layout (--sim-gather): logit err", errs, "det err", ferrs)
 
 
 def test_bench_e2e_config_matches_oracle(gpu):
