@@ -65,6 +65,12 @@ DTYPES = {"fp16x3": "f32 (fp16x3: power-of-two-scaled operands split into 2 fp16
           "bf16x6": "f32 (bf16x6: operands split into 3 bf16 terms, 6 products, f32 accumulate)",
           "f32": "f32"}
 METRIC = "BEV frames/sec (608x608, bs=16)"
+# Synthetic weights of every workload (sfa_hip.synthetic.synthetic_state_dict seed).  Seed 2, not 0:
+# on the uniform BEV frames seed 0's heatmaps put every top-51 score at the decode's 1 - 1e-4 clamp
+# (~5,000 tied peaks per frame), so its detections were a tie order and the timed batch could not be
+# compared with the reference's own detections; seed 2's top scores (~0.95) are distinct and
+# tests/golden/bench_golden.npz holds the reference's forward + decode of this exact batch.
+BENCH_WEIGHT_SEED = 2
 
 
 def parse(argv=None):
@@ -311,7 +317,7 @@ def build_pipeline(dev, args, rank, engine=None):
     if engine is None:
         arch = _lib.make_arch(DEFAULT_HEADS)
         spec = _lib.state_layout(arch)
-        sd = synthetic.synthetic_state_dict(spec, seed=0)
+        sd = synthetic.synthetic_state_dict(spec, seed=BENCH_WEIGHT_SEED)
         engine = KfpnEngine(arch, pack_state_dict(sd, arch), dev,
                             math=MATHS[args.math])
     if args.workload == "e2e":
@@ -657,7 +663,7 @@ def cpu_baseline(args, bench=None):
     threads, ncores = _cpu_threads()
     torch.set_num_threads(threads)
     arch = _lib.make_arch(DEFAULT_HEADS)
-    sd = model_oracle.state_dict_torch(synthetic.synthetic_state_dict(_lib.state_layout(arch), 0))
+    sd = model_oracle.state_dict_torch(synthetic.synthetic_state_dict(_lib.state_layout(arch), BENCH_WEIGHT_SEED))
     B = args.batch
     e2e = args.workload == "e2e"
     clouds = [synthetic.synthetic_point_cloud(i + 1) for i in range(B)] if e2e else None
@@ -735,7 +741,7 @@ def run_stream(args, rank, world, dev):
     import tempfile
     from sfa_hip.stream import StreamingDetector
     arch = _lib.make_arch(DEFAULT_HEADS)
-    sd = synthetic.synthetic_state_dict(_lib.state_layout(arch), seed=0)
+    sd = synthetic.synthetic_state_dict(_lib.state_layout(arch), seed=BENCH_WEIGHT_SEED)
     # several pipelines in flight + the copy stream: no side streams ("auto"), so every stream
     # keeps a hardware queue of its own (profiles/r02b_stream_side_streams.txt)
     side = {"on": True, "off": False, "auto": world == 1 and args.stream_inflight < 2}[args.side_streams]
@@ -788,7 +794,7 @@ def run_fusion(args, rank, world, dev):
     import project_cases
     from sfa_hip.runtime import FusionPipeline
     arch = _lib.make_arch(DEFAULT_HEADS)
-    sd = synthetic.synthetic_state_dict(_lib.state_layout(arch), seed=0)
+    sd = synthetic.synthetic_state_dict(_lib.state_layout(arch), seed=BENCH_WEIGHT_SEED)
     engine = KfpnEngine(arch, pack_state_dict(sd, arch), dev,
                         math=MATHS[args.math])
     cal = project_cases.calibs()["avg"]
@@ -958,7 +964,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": DTYPES[args.math],
-            "data": ("synthetic (hash-RNG U[0,1) BEV frames; synthetic He-uniform weights, BN folded)"
+            "data": ("synthetic (hash-RNG U[0,1) BEV frames; synthetic He-uniform weights seed %d, BN folded)" % BENCH_WEIGHT_SEED
                      if args.input == "uniform" else
                      "synthetic (BEV maps of synthetic 132,880-pt sweeps, SURVEY §8(d); synthetic weights)")
                     if args.workload == "bev_infer" else

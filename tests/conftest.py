@@ -35,6 +35,12 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def golden_bench():
+    import numpy as np
+    return np.load(os.path.join(GOLDEN, "bench_golden.npz"))
+
+
+@pytest.fixture(scope="session")
 def golden_fusion():
     import numpy as np
     return np.load(os.path.join(GOLDEN, "fusion_golden.npz"))

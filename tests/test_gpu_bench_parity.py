@@ -30,7 +30,8 @@ TOL = 1e-4
 
 def _oracle_sd():
     arch = _lib.make_arch(DEFAULT_HEADS)
-    return model_oracle.state_dict_torch(synthetic.synthetic_state_dict(_lib.state_layout(arch), seed=0))
+    return model_oracle.state_dict_torch(synthetic.synthetic_state_dict(_lib.state_layout(arch),
+                                                                        seed=bench.BENCH_WEIGHT_SEED))
 
 
 def _run_timed_config(argv, gpu, steps=4, side=True):
@@ -99,6 +100,45 @@ def test_bench_bev_infer_config_matches_oracle(gpu):
     ferrs = [_check_full_identity(p, ref, args.K) for p in b.pipes]
     np.testing.assert_array_equal(b.sim_out.cpu().numpy(), b.pipes[1].dets.cpu().numpy())
     print("bench N > 1 layout (--sim-gather): logit err", errs, "det err", ferrs)
+
+
+def test_bench_config_matches_reference_fixture(gpu, golden_bench):
+    """The timed batch against the REFERENCE itself (tests/golden/bench_golden.npz: the reference's
+    forward + _sigmoid + decode(K=50) of synthetic_bev(16, seed=1) with bench's weights), both
+    pipelines: sampled logits within 1e-4 * max(1, |ref|), per-frame head sums, every detection's
+    score within 1e-4, and full identity (class exact, all ten columns within 1e-4) on every frame
+    whose reference top-51 gaps exceed twice the score error the frame's logits allow."""
+    g = golden_bench
+    assert int(g["weight_seed"]) == bench.BENCH_WEIGHT_SEED
+    args, b = _run_timed_config([], gpu)
+    ys, xs = g["sample_yx"]
+    ref_dets = g["bench/dets"]
+    for p in b.pipes:
+        worst = 0.0
+        for h in DEFAULT_HEADS:
+            o = p.outs[h].cpu().numpy()
+            r = g[f"bench/{h}/samples"]
+            smp = o[:, :, ys, xs]
+            worst = max(worst, float(np.max(np.abs(smp - r) / np.maximum(1.0, np.abs(r)))))
+            bound = TOL * np.maximum(1.0, np.abs(o)).astype(np.float64).reshape(16, -1).sum(axis=1)
+            assert np.all(np.abs(o.astype(np.float64).reshape(16, -1).sum(axis=1) - g[f"bench/{h}/sum"]) <= bound), h
+        assert worst <= TOL, worst
+        hm_err = float(np.max(np.abs(p.outs["hm_cen"].cpu().numpy()[:, :, ys, xs] - g["bench/hm_cen/samples"])))
+        got = p.dets.cpu().numpy()
+        assert float(np.max(np.abs(np.sort(got[..., 0], axis=1) - np.sort(ref_dets[..., 0], axis=1)))) <= TOL
+        same = []
+        for f in range(16):
+            # the frame's logit error from its own top-50 scores (sorted, so a swap of neighbours
+            # does not count): score error / sigmoid' (<= 1/4) bounds it from below
+            serr = float(np.max(np.abs(np.sort(got[f, :, 0]) - np.sort(ref_dets[f, :, 0]))))
+            tol = max(serr, 0.25 * hm_err) + 2e-7
+            if float(g["bench/min_gap"][f]) > 2 * tol:
+                np.testing.assert_array_equal(got[f, :, 9], ref_dets[f, :, 9], err_msg=f"frame {f}")
+                np.testing.assert_allclose(got[f], ref_dets[f], rtol=0, atol=TOL, err_msg=f"frame {f}")
+                same.append(f)
+        print(f"timed batch vs reference fixture: max rel logit err (samples) {worst:.3g}; full identity on "
+              f"{len(same)} of 16 frames whose top-51 gaps allow it: {same}")
+        assert len(same) >= 8, same
 
 
 def test_bench_e2e_config_matches_oracle(gpu):
