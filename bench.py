@@ -483,35 +483,49 @@ def dump_gathered(args, bench, rank, world):
                  side_streams=np.int64(bench.side))
 
 
-def traffic_per_forward(args):
-    """HBM bytes of the conv launches of one forward, from the committed PMC pass
-    (tools/pmc_forward.sh -> profiles/*_pmc_forward.json; rocprofv3 cannot run inside
-    this process). Only reported for the configuration it was measured on."""
-    if args.workload != "bev_infer" or args.batch != 16:
-        return None
+def _lib_sha256():
+    import hashlib
+    with open(_lib.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def _pmc_forward_file(args):
+    """The newest committed PMC pass (tools/pmc_forward.sh -> tools/pmc_forward_summary.py ->
+    profiles/r*_pmc_forward_<math>.json) that ran THIS library build (its lib_sha256 equals the
+    loaded libsfa_hip.so's): traffic measured on other kernels is never reported.  rocprofv3 cannot
+    run inside this process, so the counters come from that separate pass of the same command."""
     import glob
     files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_forward_{args.math}.json")))
     if not files and args.math == "f32":
         files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_forward.json")))
-    if not files:
+    sha = _lib_sha256()
+    for fn in reversed(files):
+        with open(fn) as f:
+            d = json.load(f)
+        if d.get("lib_sha256") == sha:
+            return fn, d
+    return None, None
+
+
+def traffic_per_forward(args):
+    """HBM bytes of the conv launches of one forward (PMC pass of this library build), or None."""
+    if args.workload != "bev_infer" or args.batch != 16:
         return None
-    with open(files[-1]) as f:
-        return int(json.load(f)["conv_hbm_bytes_per_forward"])
+    _, d = _pmc_forward_file(args)
+    return int(d["conv_hbm_bytes_per_forward"]) if d else None
 
 
 def head_traffic_per_launch(args):
-    """HBM bytes per head launch (mean over the 3 levels) from the committed PMC pass
+    """HBM bytes per head launch (mean over the 3 levels) from the PMC pass of this library build
     (tools/pmc_forward.sh: FETCH_SIZE x2 + WRITE_SIZE per dispatch, the probe's serial forward)."""
     if args.workload != "bev_infer" or args.batch != 16 or args.math != "fp16x3":
         return None
-    import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", f"r*_pmc_forward_{args.math}.json")))
-    if not files:
+    fn, d = _pmc_forward_file(args)
+    if not d:
         return None
-    with open(files[-1]) as f:
-        per = json.load(f)["per_launch"]
-    rows = [r for r in per if r["kernel"].startswith("sfa::conv_r3_kernel<256, 320")]
-    return int(sum(r["hbm_MB"] for r in rows) * 1e6 / len(rows)) if len(rows) == 3 else None
+    rows = [r for r in d["per_launch"] if r["kernel"].startswith("sfa::conv_r3_kernel<256, 320")]
+    return {"bytes": int(sum(r["hbm_MB"] for r in rows) * 1e6 / len(rows)), "file": os.path.relpath(fn, REPO),
+            "kernel": rows[0]["kernel"]} if len(rows) == 3 else None
 
 
 def head_flop_per_launch(args):
@@ -571,12 +585,15 @@ def probe_bev(args, pipe, reps=20):
     npts = int(pipe.offsets[-1])
     algo = npts * 16 + pipe.B * 3 * 608 * 608 * 4
     ach = algo / (ms * 1e-3) / 1e9
-    traffic = None  # PMC HBM bytes per call (tools/pmc_bev.sh), for the configuration it was measured on
+    traffic = None  # PMC HBM bytes per call (tools/pmc_bev.sh) of this library build at this batch
     import glob
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_bev.json")))
-    if files and pipe.B == 16:
-        with open(files[-1]) as f:
-            traffic = int(json.load(f)["bev_hbm_bytes_per_call"])
+    sha = _lib_sha256()
+    for fn in reversed(sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_bev.json")))):
+        with open(fn) as f:
+            d = json.load(f)
+        if pipe.B == 16 and d.get("lib_sha256") == sha:
+            traffic = int(d["bev_hbm_bytes_per_call"])
+            break
     return {"bound": "hbm", "unit": "GB/s", "achieved": round(ach, 1), "peak": 8000.0,
             "frac": round(ach / 8000.0, 4), "traffic": traffic,
             "traffic_basis": "PMC 2 x FETCH_SIZE + WRITE_SIZE of one call (profiles/r*_pmc_bev.json): points read "
@@ -619,10 +636,14 @@ def roofline_line(args, heads, forward_roofline, fwd_achieved, peak, peak_basis,
         "launch_us": [round(1e3 * v, 1) for v in heads],
         "avg_launch_us": round(1e3 * sum(heads) / 3, 1),
         "algorithmic_flop_per_launch": flops,
-        "traffic": head_traffic_per_launch(args),
-        "traffic_basis": "HBM bytes per launch, mean of the 3 levels: PMC 2 x FETCH_SIZE + WRITE_SIZE "
-                         "(tools/pmc_forward.sh, profiles/r*_pmc_forward_%s.json)" % args.math,
     })
+    ht = head_traffic_per_launch(args)
+    line["traffic"] = ht["bytes"] if ht else None
+    line["traffic_basis"] = (
+        "HBM bytes per launch, mean of the 3 levels: PMC 2 x FETCH_SIZE + WRITE_SIZE of %s (tools/pmc_forward.sh "
+        "on this library build, sha256 matched; kernel %s)" % (ht["file"], ht["kernel"]) if ht else
+        "null: no committed PMC pass (profiles/r*_pmc_forward_%s.json) ran this library build "
+        "(lib_sha256 %s...)" % (args.math, _lib_sha256()[:16]))
     return line
 
 

@@ -5,7 +5,7 @@ from tools/pmc_bev.sh output -> JSON for profiles/. FETCH_SIZE doubled and WRITE
 (gfx950 corrections, MI355X_MICROARCH.md §HBM); the last call of the run is summarised.
 
   python tools/pmc_bev_summary.py gpurun_out/pmc_bev profiles/r02c_pmc_bev.json"""
-import csv, collections, json, os, re, sys
+import csv, collections, hashlib, json, os, re, sys
 
 base, out = sys.argv[1], sys.argv[2]
 KERNELS = ("bev_bin_count_kernel", "bev_bin_scan_kernel", "bev_bin_kernel", "bev_strip_kernel",
@@ -42,5 +42,9 @@ res = {"bev_hbm_bytes_per_call": int(total), "per_kernel": per,
        "method": "rocprofv3 --kernel-trace --pmc (FETCH_SIZE, WRITE_SIZE passes), bench.py --workload e2e --no-graph; "
                  "HBM = 2*FETCH_SIZE + WRITE_SIZE (KiB), last sfa_bev_voxelize call (16 sweeps)",
        "kernels": [r["kernel"] for r in per]}
+_lib = os.environ.get("SFA_HIP_LIB") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+    "lidar-image_object-detection_-fpn_resnet-yolov8_amd", "sfa", "sfa_hip", "libsfa_hip.so")
+res["lib_sha256"] = hashlib.sha256(open(_lib, "rb").read()).hexdigest()  # bench.py matches it
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
