@@ -251,6 +251,7 @@ struct ConvArgs {
   // of a tile combines the partials in the conv kernel (conv_h3_kernel.h splitk_ticket) instead of
   // splitk_reduce_kernel; null: the reduce launch
   unsigned* tile_cnt;
+  int tile_cnt_words;  // capacity of tile_cnt (words): a launch with more output tiles takes the reduce launch
   // Patch stem input (stem_patch_kernel.h): STEM_IN_NHWC4 (the voxeliser's layout), STEM_IN_NCHW3
   // (the reference's (B, 3, H, W)), STEM_IN_NCHW3_FLIP (read as torch.flip(x, [2, 3])); every
   // 16 x 16 output tile scales its fp16x3 patch by its own max |x| (no layout / amax pass).

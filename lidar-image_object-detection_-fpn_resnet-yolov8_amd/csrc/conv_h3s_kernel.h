@@ -92,6 +92,7 @@ __global__ void __launch_bounds__((BM / WM) * 64, OCC) conv_h3s_kernel(const Con
   // address arithmetic were 13 % and ~25 % of a layer1 wave's time).
   const int srow = lane >> 3;
   const int kq = (lane & 7) ^ swzA(8 * wave + srow);
+  static_assert(3 * NS <= 32 && 3 * NP <= 32, "3 row-validity bits per strip piece / pre-split group in one word");
   int s_base[NS];
   unsigned s_ok = 0;
 #pragma unroll
@@ -508,10 +509,12 @@ inline int launch_conv_h3s_cfg(const ConvArgs& a, hipStream_t st) {
   ConvArgs b = a;  // the strip rows' multiply-high divisions
   b.fd_w = make_fast_div((unsigned)g.W);
   b.fd_h = make_fast_div((unsigned)g.H);
+  // tickets only with one word per output tile in the array: else the reduce launch
+  if (ks == 1 || (long long)ceil_div(a.M, BM) * (a.N / BN) > (long long)a.tile_cnt_words) b.tile_cnt = nullptr;
   hipLaunchKernelGGL((conv_h3s_kernel<BM, BN, WM, EPI, OCC, ABL>), dim3((unsigned)nblocks), dim3((BM / WM) * 64), 0,
                      st, b);
   SFA_LAUNCH_CHECK();
-  if (ks > 1 && !a.tile_cnt) {  // the slices' partials combined by the reduce launch
+  if (ks > 1 && !b.tile_cnt) {  // the slices' partials combined by the reduce launch
     const long long nel = (long long)a.M * a.N;
     hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((nel + 1023) / 1024)), dim3(256), 0, st, a);
     SFA_LAUNCH_CHECK();

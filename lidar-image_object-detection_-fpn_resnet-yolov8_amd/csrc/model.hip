@@ -796,6 +796,7 @@ static int forward_pass(const sfa_model* m, const float* x, int in_layout, int B
       a.seg[0] = seg(xcur, B, h, w, cin, 3, stride, 1);
       io(a, xslot, -1, blk_slot(li, 0, 0));
       a.tile_cnt = TK(li, 0);
+      a.tile_cnt_words = (int)bf.tick_words;
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     {
@@ -808,6 +809,7 @@ static int forward_pass(const sfa_model* m, const float* x, int in_layout, int B
       }
       io(a, blk_slot(li, 0, 0), li > 0 ? xslot : -1, blk_slot(li, 0, 1));
       a.tile_cnt = TK(li, 1);
+      a.tile_cnt_words = (int)bf.tick_words;
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     // block 1
@@ -816,6 +818,7 @@ static int forward_pass(const sfa_model* m, const float* x, int in_layout, int B
       a.seg[0] = seg(av, B, oh, ow, planes, 3, 1, 1);
       io(a, blk_slot(li, 0, 1), -1, blk_slot(li, 1, 0));
       a.tile_cnt = TK(li, 2);
+      a.tile_cnt_words = (int)bf.tick_words;
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     {
@@ -823,6 +826,7 @@ static int forward_pass(const sfa_model* m, const float* x, int in_layout, int B
       a.seg[0] = seg(t, B, oh, ow, planes, 3, 1, 1);
       io(a, blk_slot(li, 1, 0), -1, blk_slot(li, 1, 1));
       a.tile_cnt = TK(li, 3);
+      a.tile_cnt_words = (int)bf.tick_words;
       SFA_RC(launch_conv(a, EPI_STD, m->math, st));
     }
     xcur = lv;
