@@ -7,7 +7,8 @@
 # tools/ab_lib_bits.py over the full forward, previous vs new; ab = tools/ab_env.sh bench A/B (2 x 2
 # interleaved); prof = rocprofv3 kernel trace of the serial forward for both libraries, the lines of
 # KERNEL_REGEX and the per-stage times; stamps / hstamps = the s_memtime diagnostics of the strip /
-# heads kernels (tools/stampbench, tools/headstampbench, built beforehand).
+# heads kernels (tools/stampbench, tools/headstampbench: tools/build_stamps.sh regenerates the stamped copies from
+# the product headers and builds them, beforehand).
 set -u
 export TMPDIR=/tmp
 TAG="$1"
