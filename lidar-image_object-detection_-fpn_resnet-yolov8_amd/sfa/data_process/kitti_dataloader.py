@@ -132,7 +132,10 @@ def _loader(dataset, configs, shuffle, sampler):
     on_device = bool(_cfg(configs, "bev_on_device", False))  # opt-in (module docstring)
     device = _cfg(configs, "device", None) if on_device else None
     if device is not None and torch.device(device).type != "cuda":
-        device = None
+        # the device-resident maps live on a GPU: a CPU configs.device (--no_cuda) with bev_on_device is a
+        # contradiction, not a request for the current GPU
+        raise ValueError(f"configs.bev_on_device needs a CUDA configs.device, got {device}: unset bev_on_device "
+                         "for the reference's float64 CPU maps")
     return DeviceBEVLoader(DataLoader(dataset, batch_size=configs.batch_size, shuffle=shuffle,
                                       pin_memory=configs.pin_memory, num_workers=configs.num_workers,
                                       sampler=sampler, collate_fn=bev_collate), device=device, on_device=on_device)

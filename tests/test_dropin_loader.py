@@ -53,3 +53,18 @@ def test_collate_keeps_other_fields():
     assert meta == {"img_path": ["a", "b"]}
     assert isinstance(bev, kdl.DeferredBEVBatch) and [d.flip_w for d in bev.items] == [False, True]
     assert img.shape == (2, 2, 2)
+
+
+def test_bev_on_device_with_cpu_device_refused(tmp_path, monkeypatch):
+    """configs.bev_on_device with a CPU configs.device is refused up front (no silent GPU choice)."""
+    from data_process import kitti_dataloader as kdl
+    from data_process.kitti_dataset import KittiDataset
+    monkeypatch.setattr(KittiDataset, "get_image", lc.stub_image)
+    lc.make_tree(str(tmp_path))
+    cfg = lc.configs(str(tmp_path), batch_size=2, num_workers=0)
+    cfg["bev_on_device"] = True
+    cfg["device"] = torch.device("cpu")
+    with pytest.raises(ValueError, match="bev_on_device needs a CUDA"):
+        kdl.create_test_dataloader(cfg)
+    cfg["bev_on_device"] = False  # the reference's CPU maps: still fine with a CPU device
+    assert len(kdl.create_test_dataloader(cfg)) == 3
