@@ -67,3 +67,18 @@ def test_bench_two_ranks_gather_equals_single_rank_pipelines(gpu, tmp_path):
             np.testing.assert_array_equal(dets[p, 16 * rank:16 * (rank + 1)], exp)
         del ref
         torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("workload", ["stream", "e2e"])
+def test_bench_two_ranks_other_workloads_run(gpu, workload):
+    """The other N > 1 paths of bench.py on the GPU (gloo, shared device): configs[3]'s .bin stream
+    (each batch's detections all-gathered with frame ids, -1 padding) and configs[2]'s resident sweeps;
+    both ranks finish and rank 0 prints one line with the whole-job frame count."""
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--workload", workload,
+                        "--steps", "3", "--warmup", "1", "--probe-forwards", "0", "--no-cpu-baseline"],
+                       env=_env(SFA_BENCH_SHARE_DEVICE="1", SFA_DIST_BACKEND="gloo"),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 2 and lines[0]["value"] > 0, r.stdout
+    assert lines[0]["config"]["global_batch"] == 32
