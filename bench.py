@@ -807,11 +807,11 @@ def run_stream(args, rank, world, dev):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def run_fusion(args, rank, world, dev):
-    """BASELINE configs[4]: sweeps -> BEV -> forward -> decode -> post_process -> camera boxes
-    -> association / Bayesian fusion / NMS against camera boxes, all on the GPU in one HIP
-    graph (runtime.FusionPipeline).  The camera detector (YOLOv8n) is not in this framework:
-    its boxes are synthetic inputs, 30 per frame."""
+def build_fusion(args, rank, world, dev):
+    """BASELINE configs[4]'s timed configuration: ``--inflight`` FusionPipelines (the first engine
+    and its twins: own model handle, buffers, stream and HIP graph each; side streams per
+    side_streams_for), the same sweeps and 30 synthetic camera boxes per frame.  Returns the
+    pipelines and their streams (tests/test_gpu_bench_parity.py checks them)."""
     import project_cases
     from sfa_hip.runtime import FusionPipeline
     arch = _lib.make_arch(DEFAULT_HEADS)
@@ -843,6 +843,16 @@ def run_fusion(args, rank, world, dev):
             fp.capture()
         fps.append(fp)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(nf - 1)]
+    return fps, streams, (clouds, cams, calib)
+
+
+def run_fusion(args, rank, world, dev):
+    """BASELINE configs[4]: sweeps -> BEV -> forward -> decode -> post_process -> camera boxes
+    -> association / Bayesian fusion / NMS against camera boxes, all on the GPU in one HIP
+    graph (runtime.FusionPipeline).  The camera detector (YOLOv8n) is not in this framework:
+    its boxes are synthetic inputs, 30 per frame."""
+    fps, streams, _ = build_fusion(args, rank, world, dev)
+    nf = len(fps)
 
     def step(k):
         with torch.cuda.stream(streams[k % nf]):

@@ -14,6 +14,8 @@ k % 2).  Then, for EVERY frame of BOTH pipelines:
   oracle makeBEVMap, bit-exact (NCHW3 f32, the layout the patch stem reads), and the logits vs
   the oracle forward of those maps.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -156,3 +158,37 @@ def test_bench_e2e_config_matches_oracle(gpu):
     print("bench e2e config: max rel logit err per pipeline", errs)
     ferrs = [_check_full_identity(p, ref, args.K) for p in b.pipes]
     print("bench e2e config: max abs det err vs the oracle forward's decode", ferrs)
+
+
+def test_bench_fusion_config_matches_single_eager_pipeline(gpu):
+    """configs[4] as bench.py times it (``--workload fusion --batch 8``: 3 FusionPipelines, twins of one
+    engine, side streams off, each a single-branch HIP graph, replayed in turn on 3 streams): after
+    interleaved steps, every pipeline's fused boxes / confidences / classes / sources / NMS keep equal
+    those of one eager FusionPipeline on a fresh engine (tests/test_gpu_fusion_pipeline.py pins that
+    one against the oracles).  The layout whose graphs the captured memset broke."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__))))
+    args = bench.parse(["--workload", "fusion", "--batch", "8"])
+    assert args.inflight == 3 and not args.no_graph
+    fps, streams, (clouds, cams, calib) = bench.build_fusion(args, 0, 1, gpu)
+    assert all(not fp.det.engine.side_streams for fp in fps)
+    for k in range(7):
+        with torch.cuda.stream(streams[k % 3]):
+            fps[k % 3].replay()
+    torch.cuda.synchronize()
+    arch = _lib.make_arch(DEFAULT_HEADS)
+    eng = runtime.KfpnEngine(arch, runtime.pack_state_dict(
+        synthetic.synthetic_state_dict(_lib.state_layout(arch), seed=bench.BENCH_WEIGHT_SEED), arch), gpu)
+    ref = runtime.FusionPipeline(eng, 8, [calib], K=args.K, nms=args.fusion_nms,
+                                 max_points=sum(c.shape[0] for c in clouds), conf_source=_lib.CONF_SCORE)
+    ref.set_points(clouds)
+    ref.set_camera(cams)
+    ref.run()
+    torch.cuda.synchronize()
+    want = ref.results()
+    assert sum(len(r[0]) for r in want) > 0
+    for i, fp in enumerate(fps):
+        got = fp.results()
+        for b in range(8):
+            for j, name in enumerate(("boxes", "conf", "cls", "src", "keep")):
+                np.testing.assert_array_equal(got[b][j], want[b][j], err_msg=f"pipeline {i} frame {b} {name}")
