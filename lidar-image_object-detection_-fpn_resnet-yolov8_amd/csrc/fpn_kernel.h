@@ -162,6 +162,7 @@ __global__ void __launch_bounds__(256, OCC) fpn_gemm_kernel(const ConvArgs a, in
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int c16 = lane & 15, g = lane >> 4;
+  const int bx = blockIdx.x;
   const int n0 = blockIdx.y * BN;
   const int M = a.M, P = a.OH * a.OW, nframes = (M + P - 1) / P;
 
@@ -179,13 +180,13 @@ __global__ void __launch_bounds__(256, OCC) fpn_gemm_kernel(const ConvArgs a, in
   const __amdgpu_buffer_rsrc_t rsx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.seg[0].x), (short)0,
                                                                        (int)a.seg[0].bytes, 0x00020000);
   const int bfo = c16 * BROW + ((g ^ swzB(c16)) << 4);
-  const int n_my = blockIdx.x < n_mt ? (n_mt - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
+  const int n_my = bx < n_mt ? (n_mt - 1 - bx) / (int)gridDim.x + 1 : 0;
   const int steps = n_my * NCH;
 
   r3_u32x4 ra[KC][TM][2], rb[KC][TM][2];  // A chunks, ping-pong
   auto load = [&](int step, r3_u32x4 (&r)[KC][TM][2]) {
     const int t = step / NCH, c = step - t * NCH;
-    const int m0 = ((int)blockIdx.x + t * (int)gridDim.x) * BM;
+    const int m0 = (bx + t * (int)gridDim.x) * BM;
 #pragma unroll
     for (int mi = 0; mi < TM; ++mi) {
       const int m = m0 + wave * WM + mi * 16 + c16;
@@ -202,7 +203,7 @@ __global__ void __launch_bounds__(256, OCC) fpn_gemm_kernel(const ConvArgs a, in
   float as[TM], ainv[TM];
   auto process = [&](int step, r3_u32x4 (&r)[KC][TM][2]) {
     const int t = step / NCH, c = step - t * NCH;
-    const int m0 = ((int)blockIdx.x + t * (int)gridDim.x) * BM;
+    const int m0 = (bx + t * (int)gridDim.x) * BM;
     if (c == 0) {
 #pragma unroll
       for (int mi = 0; mi < TM; ++mi) {
@@ -344,7 +345,10 @@ __global__ void __launch_bounds__(256, OCC) fpn_row_kernel(const ConvArgs a, int
   const int c16 = lane & 15, g = lane >> 4;
   const int H = a.OH, W = a.OW, Hh = H >> 1, Wh = W >> 1, N = a.N;
   const int nct = N / NB;
-  const int ct = blockIdx.x % nct, rest = blockIdx.x / nct;
+  // the nct column tiles of one segment on consecutive logical ids, i.e. on one XCD: they read the same
+  // A rows, which its L2 then serves once (round 6: blockIdx order put them on nct XCDs, nct x the reads)
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int ct = lb % nct, rest = lb / nct;
   const int b = rest / segs, sk = rest - b * segs;
   const int n0 = ct * NB;
   const int y0 = sk * H / segs, y1 = (sk + 1) * H / segs;
@@ -559,7 +563,10 @@ __global__ void __launch_bounds__(fpn_seg::NT, OCC) fpn_seg_kernel(const ConvArg
   const int c16 = lane & 15, g = lane >> 4;
   const int H = a.OH, W = a.OW, Hh = H >> 1, Wh = W >> 1, N = a.N;
   const int nct = N / NB;
-  const int ct = blockIdx.x % nct, rest = blockIdx.x / nct;
+  // the nct column tiles of one segment on consecutive logical ids, i.e. on one XCD: they read the same
+  // A rows, which its L2 then serves once (round 6: blockIdx order put them on nct XCDs, nct x the reads)
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int ct = lb % nct, rest = lb / nct;
   const int b = rest / segs, sk = rest - b * segs;
   const int n0 = ct * NB;
   const int pbeg = (sk * H / segs) * W, pend = ((sk + 1) * H / segs) * W;  // the segment's pixels

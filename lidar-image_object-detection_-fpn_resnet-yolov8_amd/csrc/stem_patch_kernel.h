@@ -548,7 +548,10 @@ __global__ void __launch_bounds__(512, 1) stem_patch_pool2_kernel(const ConvArgs
   };
 
   const int G = gridDim.x;
-  const int t0 = blockIdx.x;
+  // logical block: consecutive tiles (row neighbours, whose patches share 5 input columns and the
+  // 128-B lines of each patch row) on one XCD at the same time, so its L2 serves the shared lines once
+  // (round 6: in blockIdx order neighbours ran on different XCDs)
+  const int t0 = xcd_remap(blockIdx.x, G);
   if (t0 < ntiles) fetch(t0, R0);
   if (t0 + G < ntiles) fetch(t0 + G, R1);
   // weights: wh [2][64][Kpad], k = (kh 7 + kw) 4 + c  ->  LDS [2][64][WROW] at k' = (kh 8 + kw) 4 + c
